@@ -1,0 +1,157 @@
+/*
+ * nekkrylov.h — C ABI of the MI355X (gfx950) Krylov hot path for nekStab.
+ *
+ * This is the drop-in boundary.  Everything below takes plain device pointers,
+ * sizes and a HIP stream (as `void*`), returns an `int` status, and never
+ * synchronises the host except where stated.  The reference interfaces each
+ * entry point replaces are cited as `file:line` into nekStab_next
+ * (reference @ 2025-02-27); see INTEGRATION.md for the Fortran `bind(C)`
+ * interface block a nekStab maintainer would add.
+ *
+ * ---------------------------------------------------------------------------
+ * State-vector layout (one nekStab `krylov_vector` / `real_nek_vector`,
+ * core/krylov_subspace.f90:12-17, core/nek_vectors.f90:20-31), fp64 in HBM:
+ *
+ *   [ wf_0 | wf_1 | ... | wf_{n_wf-1} | pr | time | pad ]
+ *     each wf_f is `sv` doubles: n_v live points + zero padding
+ *     pr is `sp` doubles: n_p live points + zero padding
+ *     time is one double at offset  nkv_time_offset(L) = n_wf*sv + sp
+ *
+ * Weighted fields are vx, vy, [vz], [t_1 .. t_s] — exactly the fields that
+ * enter `glsc3(.., bm1s, .., n)` in k_dot / real_dot
+ * (krylov_subspace.f90:40-50, nek_vectors.f90:94-104).  Pressure is stored
+ * and is touched by every BLAS-1 op (nopaxpby/nopcmult/..., nek_vectors.f90:
+ * 229-362) but never enters a dot.  `time` is the scalar component of the
+ * vector (krylov_subspace.f90:16).
+ *
+ * sv and sp are multiples of NKV_TILE (padding rows are zero and their
+ * weight is zero), so every kernel streams whole tiles without masking.
+ * A Krylov basis is (k+1) vectors at stride `ld` doubles (ld >= time offset+1,
+ * multiple of NKV_TILE): Q[c] = Q + c*ld.
+ *
+ * The weight vector `w` (bm1s, core/NEKSTAB:86-89; zeroed inside a sponge by
+ * core/forcing.f90:101-104) has `sv` doubles, shared by every weighted field.
+ *
+ * Multi-GPU: each rank holds an element-contiguous shard (same layout, local
+ * n_v/n_p).  Every reduction entry point writes the LOCAL partial sum to a
+ * device buffer; the caller all-reduces it (RCCL) before the consuming entry
+ * point runs on the same stream — the MI355X replacement of the per-field
+ * MPI_Allreduce hidden in Nek5000's glsc3.
+ * ------------------------------------------------------------------------- */
+#ifndef NEKKRYLOV_H
+#define NEKKRYLOV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NKV_ABI_VERSION 1
+
+/* Rows per tile: fields are padded to a multiple of this many doubles. */
+#define NKV_TILE 2048
+
+/* Status codes (every entry point). */
+#define NKV_OK 0
+#define NKV_EINVAL 1 /* bad argument / shape                          */
+#define NKV_EHIP 2   /* HIP runtime error (see nkv_last_error)        */
+#define NKV_ENAN 3   /* NaN detected in a reduction (k_dot :57 guard)  */
+#define NKV_ESHAPE 4 /* layout not padded/aligned as documented above  */
+
+/* Flags. */
+#define NKV_TIME 0x1u      /* include the `time` slot (dot: add p.time*q.time; BLAS-1: update it) */
+#define NKV_ACCUMULATE 0x2u /* block_update: f <- f - Q h   (default)                             */
+#define NKV_OVERWRITE 0x4u  /* block_update: f <- + Q h     (k_matmul, krylov_subspace.f90:163)    */
+#define NKV_NORM2 0x8u      /* block_update: also write the local ||f||_W^2 partial               */
+
+typedef struct nkv_layout {
+    int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */
+    int64_t n_p;  /* live pressure points on this rank (lx2*ly2*lz2*nelv; 0: no pr)  */
+    int64_t sv;   /* padded stride of one weighted field (multiple of NKV_TILE)     */
+    int64_t sp;   /* padded length of the pressure segment (multiple of NKV_TILE)   */
+    int64_t ld;   /* stride between basis vectors, doubles (multiple of NKV_TILE)   */
+    int32_t n_wf; /* number of weighted fields: 2 or 3 velocities + active scalars  */
+    int32_t rank0;/* 1 on the rank that owns the replicated `time` term of a dot    */
+} nkv_layout;
+
+/* ---- runtime ---------------------------------------------------------- */
+int nkv_abi_version(void);
+const char* nkv_last_error(void);
+/* Device properties of the current HIP device (host sync-free). */
+int nkv_device_info(int* device, int* cu_count, int64_t* hbm_bytes, char* name, int name_len);
+/* Bytes of device scratch the reduction entry points need for up to `max_cols` columns. */
+size_t nkv_workspace_bytes(const nkv_layout* L, int max_cols);
+/* Reads (with a stream sync) and clears the NaN flag kept in the workspace. */
+int nkv_check_status(void* ws, void* stream);
+
+/* ---- BLAS-1 over all stored fields (a5/a6) ----------------------------------------------
+ * k_zero/real_zero        krylov_subspace.f90:141-150, nek_vectors.f90:70-78
+ * k_copy                  krylov_subspace.f90:152-161
+ * k_cmult/real_scal       krylov_subspace.f90:94-104,  nek_vectors.f90:116-125
+ * real_axpby (time NOT updated unless NKV_TIME)           nek_vectors.f90:127-139,257-277
+ * k_add2/k_sub2 = axpby(1,±1), k_sub3                     krylov_subspace.f90:106-139 */
+int nkv_zero(const nkv_layout* L, double* x, unsigned flags, void* stream);
+int nkv_copy(const nkv_layout* L, double* dst, const double* src, unsigned flags, void* stream);
+int nkv_scal(const nkv_layout* L, double* x, double alpha, unsigned flags, void* stream);
+int nkv_axpby(const nkv_layout* L, double* x, double alpha, const double* y, double beta,
+              unsigned flags, void* stream);
+int nkv_sub3(const nkv_layout* L, double* p, const double* q, const double* r, unsigned flags,
+             void* stream);
+/* x <- x + sign * (*alpha_dev) * y, the scalar read on the device (MGS step, stream-ordered). */
+int nkv_axpy_dev(const nkv_layout* L, double* x, const double* alpha_dev, double sign, const double* y,
+                 unsigned flags, void* stream);
+/* x <- x / sqrt(*nrm2_dev)   (k_normalize, krylov_subspace.f90:75-92); writes sqrt to beta_dev. */
+int nkv_normalize_dev(const nkv_layout* L, double* x, const double* nrm2_dev, double* beta_dev,
+                      unsigned flags, void* stream);
+
+/* ---- weighted inner product (a1-a3) -------------------------------------------------------
+ * out_dev[0] = sum_fields sum_i a_i*w_i*b_i (+ a.time*b.time if NKV_TIME and rank0)
+ * k_dot krylov_subspace.f90:26-60 (time only when uparam(1)==2.1), real_dot nek_vectors.f90:80-114
+ * (time always), inner_product eigensolvers.f90:3-56, glsc3 [Nek5000].  LOCAL partial. */
+int nkv_dot(const nkv_layout* L, const double* w, const double* a, const double* b, double* out_dev,
+            void* ws, unsigned flags, void* stream);
+
+/* ---- block Gram–Schmidt (a7, update_hessenberg_matrix krylov_decomposition.f90:103-189) ----
+ * block_dot:    h_dev[0:j] = Q[:,0:j]^T W f  (LOCAL partials, deterministic 2-stage reduction)
+ * block_update: f <- f - Q[:,0:j] h           (NKV_ACCUMULATE, default)
+ *               f <- Q[:,0:j] h               (NKV_OVERWRITE: k_matmul / mode reconstruction)
+ *               with NKV_NORM2 also nrm2_dev[0] = ||f_new||_W^2 local partial (+time term)
+ * arnoldi_finish: q_out = f/beta, beta = sqrt(nrm2_dev[0]); H column k written on the device:
+ *               hcol[i] = h1[i] + h2[i] (i<j; h2 may be NULL), hcol[j] = beta (H(k+1,k), :183-186) */
+int nkv_block_dot(const nkv_layout* L, const double* w, const double* Q, int j, const double* f,
+                  double* h_dev, void* ws, unsigned flags, void* stream);
+int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
+                     double* f, double* nrm2_dev, void* ws, unsigned flags, void* stream);
+int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,
+                       int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
+                       unsigned flags, void* stream);
+
+/* ---- Krylov–Schur restart (a10, schur_condensation eigensolvers.f90:421-442) --------------
+ * In place: Q[:,0:k] <- Q[:,0:k] * V, V k-by-k column-major (leading dim ldv) in device memory.
+ * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 256. */
+int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream);
+
+/* ---- synthetic operators (the matvec boundary, linear_operators.f90:17-23) ----------------
+ * op_diag: y = d .* x over every stored row; y.time = time_scale * x.time.
+ * op_rot2: per weighted point i, (u,v) = (wf_0[i], wf_1[i]):
+ *          y = [[c_i, -s_i],[s_i, c_i]] (u,v)   (transpose: s -> -s), other weighted fields and
+ *          pressure multiplied by d_rest[row] (may be NULL → 0), y.time = 0. */
+int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y, double time_scale,
+                void* stream);
+int nkv_op_rot2(const nkv_layout* L, const double* c, const double* s, const double* d_rest,
+                const double* x, double* y, int transpose, void* stream);
+
+/* ---- shard-independent synthetic data ----------------------------------------------------
+ * x[row] = 2*u - 1, u = hash(seed, field, global point) in [0,1) with 53 exact bits, for live
+ * rows; padding rows = 0; time = 0.  Global point of local point i in a weighted field is
+ * v_offset + i, in pressure p_offset + i (element-contiguous shards).  Bit-identical to the
+ * oracle's generator for every shard split. */
+int nkv_fill_hash(const nkv_layout* L, double* x, uint64_t seed, int64_t v_offset, int64_t p_offset,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEKKRYLOV_H */

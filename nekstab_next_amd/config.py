@@ -1,0 +1,26 @@
+"""Solver knobs with nekStab's defaults (core/main.f90:9-16, core/NEKSTAB:37-42)."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass
+class KrylovSchurConfig:
+    k_dim: int = 100          # Krylov subspace dimension (k_dim, main.f90:9)
+    schur_tgt: int = 2        # wanted converged eigenvalues; <= 0: plain k-step Arnoldi (:10, :314-317)
+    eigen_tol: float = 1e-6   # Ritz residual tolerance (:11)
+    schur_del: float = 0.1    # keep |lambda| >= 1 - schur_del at restarts (:12)
+    maxmodes: int = 20        # max eigenmodes exported (:13)
+    mode: str = "cgs2"        # "cgs2" (block, MI355X hot path) | "mgs2" (reference operation order)
+    seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "as_is"
+    faithful_select: bool = True   # reproduce quicksort2's ordering quirk
+    max_restarts: int = 1000       # the reference loops until converged; this bounds it
+
+
+@dataclass
+class GmresConfig:
+    k_dim: int = 100          # inner Krylov dimension (ksize)
+    maxiter: int = 100        # restarts (newton_krylov.f90:120: ts_gmres(f, dq, 100, k_dim, calls))
+    tol: float = 1e-9         # max(param(21), param(22)) (newton_krylov.f90:236); test on beta**2
+    mode: str = "cgs2"
+    findiff: bool = False     # iffindiff relaxed exits (1e-8 inner, 1e-6 outer; :269, :292)

@@ -1,0 +1,796 @@
+// nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
+//
+// Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
+// Design notes (roofline, bytes per launch): DESIGN.md.
+//
+// Every kernel here is HBM-bound fp64 streaming (BLAS-1/2): 16-B (double2) coalesced loads,
+// 256-thread workgroups (4 wave64s), wave reductions by cross-lane shuffles, LDS for the
+// per-workgroup partials, and a deterministic two-stage reduction (fixed block->tile map,
+// fixed-order second stage; no floating-point atomics) so results do not depend on timing.
+// The one near-ridge kernel (restart rotation Q <- Q V) is LDS-tiled with 4x4 register blocks.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "nekkrylov.h"
+
+namespace {
+
+constexpr int kThreads = 256;                       // 4 waves of 64
+constexpr int kPairs = 4;                            // double2 per thread per tile
+constexpr int kTile = kThreads * kPairs * 2;         // 2048 rows per tile
+static_assert(kTile == NKV_TILE, "tile size must match the documented padding");
+constexpr int kMaxBlocks = 2048;                     // reduction partial slots per column
+constexpr int kColUnroll = 4;                        // columns in flight per thread (block dot)
+constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
+constexpr int kRotRows = 64;                         // rows per rotation tile
+constexpr int kRotMaxK = 256;
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define NKV_HIP(call)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(NKV_EHIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__,  \
+                        __LINE__);                                                           \
+    } while (0)
+
+#define NKV_LAUNCHED()                                                                       \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess)                                                                \
+            return fail(NKV_EHIP, "kernel launch: %s (%s:%d)", hipGetErrorString(e_),        \
+                        __FILE__, __LINE__);                                                 \
+    } while (0)
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Rows that every BLAS-1 op streams (weighted fields + pressure, padded); the time slot sits at
+// this offset.
+inline int64_t rows_of(const nkv_layout* L) { return (int64_t)L->n_wf * L->sv + L->sp; }
+
+int check_layout(const nkv_layout* L) {
+    if (!L) return fail(NKV_EINVAL, "layout is NULL");
+    if (L->n_wf < 1 || L->n_v < 0 || L->n_p < 0)
+        return fail(NKV_EINVAL, "bad layout: n_wf=%d n_v=%lld n_p=%lld", L->n_wf,
+                    (long long)L->n_v, (long long)L->n_p);
+    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % kTile || L->sp % kTile || L->ld % kTile)
+        return fail(NKV_ESHAPE, "layout not padded to NKV_TILE: sv=%lld sp=%lld ld=%lld",
+                    (long long)L->sv, (long long)L->sp, (long long)L->ld);
+    if (L->ld < rows_of(L) + 1)
+        return fail(NKV_ESHAPE, "ld=%lld too small for %lld rows + time", (long long)L->ld,
+                    (long long)rows_of(L));
+    return NKV_OK;
+}
+
+int check_ptr(const void* p, const char* what) {
+    if (!p) return fail(NKV_EINVAL, "%s is NULL", what);
+    if (reinterpret_cast<uintptr_t>(p) % 16) return fail(NKV_ESHAPE, "%s not 16-byte aligned", what);
+    return NKV_OK;
+}
+
+#define CHECK(x)                   \
+    do {                           \
+        int rc_ = (x);             \
+        if (rc_ != NKV_OK) return rc_; \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Block-wide sum of one double (256 threads); result valid in thread 0.
+__device__ __forceinline__ double block_sum(double v, double* lds4) {
+    v = wave_sum(v);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) lds4[wave] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+    return r;
+}
+
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+
+// ------------------------------------------------------------------------------------------
+// block weighted multi-dot:  partials[c][b] = sum over this block's tiles of q_c . (w f)
+// grid = (bx, n_wf): blockIdx.y is the weighted field, so the weight index is the row within
+// the field (no per-element division).  Each thread keeps its 8 rows of w.f in registers and
+// streams the j basis columns past them, kColUnroll columns in flight.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict__ Q, int64_t ld,
+                                                        int j, const double* __restrict__ f,
+                                                        const double* __restrict__ w, int64_t sv,
+                                                        int tiles_per_field,
+                                                        double* __restrict__ partials, int B) {
+    extern __shared__ double red[];  // [4 waves][j]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = threadIdx.x; c < 4 * j; c += kThreads) red[c] = 0.0;
+    __syncthreads();
+
+    const int64_t fb = (int64_t)blockIdx.y * sv;
+    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 wf[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 wv = ld2(w + r0 + k * 2 * kThreads);
+            const double2 fv = ld2(f + fb + r0 + k * 2 * kThreads);
+            wf[k].x = wv.x * fv.x;
+            wf[k].y = wv.y * fv.y;
+        }
+        const double* qb = Q + fb + r0;
+        int c = 0;
+        for (; c + kColUnroll <= j; c += kColUnroll) {
+            double2 q[kColUnroll][kPairs];
+#pragma unroll
+            for (int u = 0; u < kColUnroll; ++u)
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ld2(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+            double s[kColUnroll];
+#pragma unroll
+            for (int u = 0; u < kColUnroll; ++u) {
+                double a = 0.0;
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    a = fma(q[u][k].x, wf[k].x, a);
+                    a = fma(q[u][k].y, wf[k].y, a);
+                }
+                s[u] = a;
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+                for (int u = 0; u < kColUnroll; ++u) s[u] += __shfl_xor(s[u], off, 64);
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < kColUnroll; ++u) red[wave * j + c + u] += s[u];
+            }
+        }
+        for (; c < j; ++c) {
+            double a = 0.0;
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 q = ld2(qb + (int64_t)c * ld + k * 2 * kThreads);
+                a = fma(q.x, wf[k].x, a);
+                a = fma(q.y, wf[k].y, a);
+            }
+            a = wave_sum(a);
+            if (lane == 0) red[wave * j + c] += a;
+        }
+    }
+    __syncthreads();
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    for (int c = threadIdx.x; c < j; c += kThreads)
+        partials[(int64_t)c * B + b] = (red[c] + red[j + c]) + (red[2 * j + c] + red[3 * j + c]);
+}
+
+// Second stage: out[c] = sum_b partials[c][b] in a fixed order (+ replicated time term).
+__global__ __launch_bounds__(kThreads) void k_reduce_cols(const double* __restrict__ partials, int B,
+                                                          double* __restrict__ out,
+                                                          const double* __restrict__ ta, int64_t lda,
+                                                          const double* __restrict__ tb,
+                                                          int* __restrict__ nan_flag) {
+    __shared__ double lds4[4];
+    const int c = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < B; b += kThreads) s += partials[(int64_t)c * B + b];
+    s = block_sum(s, lds4);
+    if (threadIdx.x == 0) {
+        if (ta) s += ta[(int64_t)c * lda] * tb[0];
+        if (s != s) atomicOr(nan_flag, 1);
+        out[c] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// block update:  f <- f - Q h  (or f <- Q h), optional fused ||f_new||_W^2 partial.
+// 1-D grid-stride over all tiles of the vector; a tile never straddles fields (sv, sp are
+// multiples of the tile), so the weight row is r - field*sv.
+// ------------------------------------------------------------------------------------------
+template <bool OVERWRITE, bool NORM>
+__global__ __launch_bounds__(kThreads) void k_block_update(const double* __restrict__ Q, int64_t ld,
+                                                           int j, const double* __restrict__ h,
+                                                           double* __restrict__ f,
+                                                           const double* __restrict__ w, int64_t sv,
+                                                           int tiles_per_field, int tiles_w,
+                                                           int tiles_total, int64_t time_off,
+                                                           int do_time,
+                                                           double* __restrict__ partials) {
+    __shared__ double lds4[4];
+    // time slot (one double): wave 0 of block 0, lanes split the columns.
+    if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
+        double s = 0.0;
+        for (int c = threadIdx.x; c < j; c += 64) s = fma(Q[time_off + (int64_t)c * ld], h[c], s);
+        s = wave_sum(s);
+        if (threadIdx.x == 0) f[time_off] = OVERWRITE ? s : f[time_off] - s;
+    }
+    double nrm = 0.0;
+    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 acc[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            if (OVERWRITE) acc[k] = make_double2(0.0, 0.0);
+            else acc[k] = ld2(f + r0 + k * 2 * kThreads);
+        }
+        const double* qb = Q + r0;
+        int c = 0;
+        for (; c + 4 <= j; c += 4) {
+            double2 q[4][kPairs];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ld2(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double hc = OVERWRITE ? h[c + u] : -h[c + u];
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    acc[k].x = fma(hc, q[u][k].x, acc[k].x);
+                    acc[k].y = fma(hc, q[u][k].y, acc[k].y);
+                }
+            }
+        }
+        for (; c < j; ++c) {
+            const double hc = OVERWRITE ? h[c] : -h[c];
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 q = ld2(qb + (int64_t)c * ld + k * 2 * kThreads);
+                acc[k].x = fma(hc, q.x, acc[k].x);
+                acc[k].y = fma(hc, q.y, acc[k].y);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) st2(f + r0 + k * 2 * kThreads, acc[k]);
+        if (NORM && t < tiles_w) {
+            const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 wv = ld2(w + wr + k * 2 * kThreads);
+                nrm = fma(wv.x * acc[k].x, acc[k].x, nrm);
+                nrm = fma(wv.y * acc[k].y, acc[k].y, nrm);
+            }
+        }
+    }
+    if (NORM) {
+        nrm = block_sum(nrm, lds4);
+        if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Arnoldi finish / normalise:  q = f / sqrt(nrm2)  (all rows + time), H column on the device.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_finish(const double* f,  // may alias q (in-place)
+                                                     const double* __restrict__ nrm2,
+                                                     double* q, int64_t rows,
+                                                     int64_t time_off, int j,
+                                                     const double* __restrict__ h1,
+                                                     const double* __restrict__ h2,
+                                                     double* __restrict__ hcol,
+                                                     double* __restrict__ beta_out) {
+    const double beta = sqrt(nrm2[0]);
+    const double inv = 1.0 / beta;  // k_normalize: inv_alpha = 1/alpha; k_cmult (krylov_subspace.f90:87-90)
+    const int64_t pairs = rows / 2;
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs;
+         p += (int64_t)gridDim.x * kThreads) {
+        double2 v = ld2(f + 2 * p);
+        v.x *= inv;
+        v.y *= inv;
+        st2(q + 2 * p, v);
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            q[time_off] = f[time_off] * inv;
+            if (beta_out) beta_out[0] = beta;
+        }
+        if (hcol) {
+            for (int i = threadIdx.x; i < j; i += kThreads) hcol[i] = h1[i] + (h2 ? h2[i] : 0.0);
+            if (threadIdx.x == 0) hcol[j] = beta;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// BLAS-1 family (one kernel, op selected per launch):  rows [0, rows) as double2 + time slot.
+// ------------------------------------------------------------------------------------------
+enum Op : int { OP_ZERO = 0, OP_COPY, OP_SCAL, OP_AXPBY, OP_SUB3, OP_AXPY_DEV };
+
+template <int OP>
+__global__ __launch_bounds__(kThreads) void k_blas1(double* x, const double* y,  // may alias
+                                                    const double* z, double a, double b,
+                                                    const double* __restrict__ a_dev, int64_t rows,
+                                                    int64_t time_off, int do_time) {
+    if (OP == OP_AXPY_DEV) a = b * a_dev[0];
+    const int64_t pairs = rows / 2;
+    const int64_t n = do_time ? pairs + 1 : pairs;  // last "pair" index = the time slot
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n;
+         p += (int64_t)gridDim.x * kThreads) {
+        if (p == pairs) {  // scalar time component
+            const int64_t i = time_off;
+            if (OP == OP_ZERO) x[i] = 0.0;
+            if (OP == OP_COPY) x[i] = y[i];
+            if (OP == OP_SCAL) x[i] = x[i] * a;
+            if (OP == OP_AXPBY) x[i] = x[i] * a + y[i] * b;
+            if (OP == OP_SUB3) x[i] = y[i] - z[i];
+            if (OP == OP_AXPY_DEV) x[i] = fma(a, y[i], x[i]);
+            continue;
+        }
+        const int64_t i = 2 * p;
+        double2 r;
+        if (OP == OP_ZERO) r = make_double2(0.0, 0.0);
+        if (OP == OP_COPY) r = ld2(y + i);
+        if (OP == OP_SCAL) {
+            r = ld2(x + i);
+            r.x *= a;
+            r.y *= a;
+        }
+        if (OP == OP_AXPBY) {  // nek axpby: x(i) = x(i)*alpha + y(i)*beta (nek_vectors.f90:250-256)
+            const double2 xv = ld2(x + i), yv = ld2(y + i);
+            r.x = xv.x * a + yv.x * b;
+            r.y = xv.y * a + yv.y * b;
+        }
+        if (OP == OP_SUB3) {
+            const double2 yv = ld2(y + i), zv = ld2(z + i);
+            r.x = yv.x - zv.x;
+            r.y = yv.y - zv.y;
+        }
+        if (OP == OP_AXPY_DEV) {
+            const double2 xv = ld2(x + i), yv = ld2(y + i);
+            r.x = fma(a, yv.x, xv.x);
+            r.y = fma(a, yv.y, xv.y);
+        }
+        st2(x + i, r);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Restart rotation, in place:  Q[:, 0:k] <- Q[:, 0:k] V.   One workgroup owns 64 rows: the
+// 64 x k input tile is staged in LDS (so outputs can overwrite those rows), V streams through
+// LDS in 16 x 64 chunks, each thread accumulates a 4 x 4 register block.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_rotate(double* __restrict__ Q, int64_t ld, int k,
+                                                     const double* __restrict__ V, int ldv,
+                                                     int64_t n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* A = sm;                 // [k][kRotRows]
+    double* Vs = sm + k * kRotRows;  // [16][64]
+    const int tr = threadIdx.x & 15;  // rows 4*tr .. 4*tr+3
+    const int tc = threadIdx.x >> 4;  // cols 4*tc .. 4*tc+3 of the current 64-column chunk
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t row0 = tile * kRotRows;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < k * (kRotRows / 2); idx += kThreads) {
+            const int c = idx / (kRotRows / 2), r2 = idx % (kRotRows / 2);
+            st2(A + c * kRotRows + 2 * r2, ld2(Q + (int64_t)c * ld + row0 + 2 * r2));
+        }
+        __syncthreads();
+        for (int cc = 0; cc < k; cc += 64) {
+            double acc[4][4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+            for (int ii = 0; ii < k; ii += 16) {
+                for (int e = threadIdx.x; e < 16 * 64; e += kThreads) {
+                    const int i = e >> 6, c = e & 63;
+                    const int gi = ii + i, gc = cc + c;
+                    Vs[e] = (gi < k && gc < k) ? V[gi + (int64_t)gc * ldv] : 0.0;
+                }
+                __syncthreads();
+                const int imax = min(16, k - ii);
+                for (int i = 0; i < imax; ++i) {
+                    const double2 a01 = ld2(A + (ii + i) * kRotRows + 4 * tr);
+                    const double2 a23 = ld2(A + (ii + i) * kRotRows + 4 * tr + 2);
+                    const double2 v01 = ld2(Vs + i * 64 + 4 * tc);
+                    const double2 v23 = ld2(Vs + i * 64 + 4 * tc + 2);
+                    const double av[4] = {a01.x, a01.y, a23.x, a23.y};
+                    const double vv[4] = {v01.x, v01.y, v23.x, v23.y};
+#pragma unroll
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) acc[a][b] = fma(av[a], vv[b], acc[a][b]);
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int gc = cc + 4 * tc + b;
+                if (gc < k) {
+                    double* dst = Q + (int64_t)gc * ld + row0 + 4 * tr;
+                    st2(dst, make_double2(acc[0][b], acc[1][b]));
+                    st2(dst + 2, make_double2(acc[2][b], acc[3][b]));
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic operators and data
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__ d,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ y, int64_t rows,
+                                                      int64_t time_off, double ts) {
+    const int64_t pairs = rows / 2;
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs;
+         p += (int64_t)gridDim.x * kThreads) {
+        const double2 dv = ld2(d + 2 * p), xv = ld2(x + 2 * p);
+        st2(y + 2 * p, make_double2(dv.x * xv.x, dv.y * xv.y));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
+}
+
+__global__ __launch_bounds__(kThreads) void k_op_rot2(const double* __restrict__ cs,
+                                                      const double* __restrict__ sn,
+                                                      const double* __restrict__ dr,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ y, int64_t sv,
+                                                      int64_t rows, int64_t time_off, double sgn) {
+    const int64_t pairs = rows / 2;
+    const int64_t pv = sv / 2;
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs;
+         p += (int64_t)gridDim.x * kThreads) {
+        if (p < pv) {  // (u, v) = (field 0, field 1) at the same point
+            const double2 c = ld2(cs + 2 * p), s = ld2(sn + 2 * p);
+            const double2 u = ld2(x + 2 * p), v = ld2(x + sv + 2 * p);
+            st2(y + 2 * p, make_double2(c.x * u.x - sgn * s.x * v.x, c.y * u.y - sgn * s.y * v.y));
+            st2(y + sv + 2 * p, make_double2(sgn * s.x * u.x + c.x * v.x, sgn * s.y * u.y + c.y * v.y));
+        } else if (p >= 2 * pv) {
+            const double2 xv = ld2(x + 2 * p);
+            const double2 dv = dr ? ld2(dr + 2 * p) : make_double2(0.0, 0.0);
+            st2(y + 2 * p, make_double2(dv.x * xv.x, dv.y * xv.y));
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = 0.0;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void k_fill_hash(double* __restrict__ x, uint64_t seed,
+                                                        int n_wf, int64_t n_v, int64_t sv,
+                                                        int64_t n_p, int64_t rows,
+                                                        int64_t time_off, int64_t voff,
+                                                        int64_t poff) {
+    const uint64_t key0 = seed * 0xD1342543DE82EF95ull;
+    for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < rows;
+         r += (int64_t)gridDim.x * kThreads) {
+        int64_t field = r / sv, i = r - field * sv;
+        bool live;
+        uint64_t gp, fid;
+        if (field < n_wf) {
+            live = i < n_v;
+            gp = (uint64_t)(voff + i);
+            fid = (uint64_t)field;
+        } else {
+            i = r - (int64_t)n_wf * sv;
+            live = i < n_p;
+            gp = (uint64_t)(poff + i);
+            fid = 31ull;
+        }
+        double v = 0.0;
+        if (live) {
+            const uint64_t z = mix64(key0 + fid * 0x9E3779B97F4A7C15ull + gp);
+            const double u = (double)(z >> 11) * 0x1.0p-53;
+            v = 2.0 * u - 1.0;
+        }
+        x[r] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) x[time_off] = 0.0;
+}
+
+int grid_for(int64_t work_items, int cap = 4096) {
+    int64_t g = (work_items + kThreads - 1) / kThreads;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+struct Ctrl {
+    int nan_flag;
+};
+
+inline int* nan_flag_of(void* ws) { return &reinterpret_cast<Ctrl*>(ws)->nan_flag; }
+inline double* partials_of(void* ws) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + kCtrlBytes);
+}
+
+// Shared launcher for block dots (nkv_dot is the j = 1 case).
+int launch_block_dot(const nkv_layout* L, const double* w, const double* Q, int64_t ld, int j,
+                     const double* f, double* out, void* ws, unsigned flags, hipStream_t st) {
+    const int tpf = (int)(L->sv / kTile);
+    int bx = kMaxBlocks / L->n_wf;
+    if (bx > tpf) bx = tpf;
+    if (bx < 1) bx = 1;
+    const int B = bx * L->n_wf;
+    double* part = partials_of(ws);
+    if (tpf > 0) {
+        hipLaunchKernelGGL(k_block_dot, dim3(bx, L->n_wf), dim3(kThreads), 4 * j * sizeof(double), st,
+                           Q, ld, j, f, w, L->sv, tpf, part, B);
+        NKV_LAUNCHED();
+    }
+    const int64_t T = rows_of(L);
+    const bool tdot = (flags & NKV_TIME) && L->rank0;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, out,
+                       tdot ? Q + T : nullptr, ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI
+// ==========================================================================================
+extern "C" {
+
+int nkv_abi_version(void) { return NKV_ABI_VERSION; }
+
+const char* nkv_last_error(void) { return g_err; }
+
+int nkv_device_info(int* device, int* cu_count, int64_t* hbm_bytes, char* name, int name_len) {
+    int dev = 0;
+    NKV_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    NKV_HIP(hipGetDeviceProperties(&p, dev));
+    if (device) *device = dev;
+    if (cu_count) *cu_count = p.multiProcessorCount;
+    if (hbm_bytes) *hbm_bytes = (int64_t)p.totalGlobalMem;
+    if (name && name_len > 0) {
+        snprintf(name, name_len, "%s", p.gcnArchName);
+    }
+    return NKV_OK;
+}
+
+size_t nkv_workspace_bytes(const nkv_layout* L, int max_cols) {
+    (void)L;
+    if (max_cols < 1) max_cols = 1;
+    return kCtrlBytes + (size_t)kMaxBlocks * (size_t)(max_cols + 1) * sizeof(double);
+}
+
+int nkv_check_status(void* ws, void* stream) {
+    CHECK(check_ptr(ws, "ws"));
+    int flag = 0;
+    NKV_HIP(hipMemcpyAsync(&flag, nan_flag_of(ws), sizeof(int), hipMemcpyDeviceToHost, S(stream)));
+    NKV_HIP(hipStreamSynchronize(S(stream)));
+    if (flag) {
+        NKV_HIP(hipMemsetAsync(nan_flag_of(ws), 0, sizeof(int), S(stream)));
+        return fail(NKV_ENAN, "NaN detected in dot product");  // nek_vectors.f90:108-111
+    }
+    return NKV_OK;
+}
+
+static int blas1(const nkv_layout* L, int op, double* x, const double* y, const double* z, double a,
+                 double b, const double* a_dev, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(x, "x"));
+    const int64_t rows = rows_of(L);
+    const int g = grid_for(rows / 2 + 1);
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    hipStream_t st = S(stream);
+    switch (op) {
+        case OP_ZERO: hipLaunchKernelGGL(k_blas1<OP_ZERO>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        case OP_COPY: hipLaunchKernelGGL(k_blas1<OP_COPY>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        case OP_SCAL: hipLaunchKernelGGL(k_blas1<OP_SCAL>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        case OP_AXPBY: hipLaunchKernelGGL(k_blas1<OP_AXPBY>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        case OP_SUB3: hipLaunchKernelGGL(k_blas1<OP_SUB3>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        case OP_AXPY_DEV: hipLaunchKernelGGL(k_blas1<OP_AXPY_DEV>, dim3(g), dim3(kThreads), 0, st, x, y, z, a, b, a_dev, rows, rows, dt); break;
+        default: return fail(NKV_EINVAL, "bad op");
+    }
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_zero(const nkv_layout* L, double* x, unsigned flags, void* stream) {
+    return blas1(L, OP_ZERO, x, nullptr, nullptr, 0, 0, nullptr, flags, stream);
+}
+int nkv_copy(const nkv_layout* L, double* dst, const double* src, unsigned flags, void* stream) {
+    CHECK(check_ptr(src, "src"));
+    return blas1(L, OP_COPY, dst, src, nullptr, 0, 0, nullptr, flags, stream);
+}
+int nkv_scal(const nkv_layout* L, double* x, double alpha, unsigned flags, void* stream) {
+    return blas1(L, OP_SCAL, x, nullptr, nullptr, alpha, 0, nullptr, flags, stream);
+}
+int nkv_axpby(const nkv_layout* L, double* x, double alpha, const double* y, double beta,
+              unsigned flags, void* stream) {
+    CHECK(check_ptr(y, "y"));
+    return blas1(L, OP_AXPBY, x, y, nullptr, alpha, beta, nullptr, flags, stream);
+}
+int nkv_sub3(const nkv_layout* L, double* p, const double* q, const double* r, unsigned flags,
+             void* stream) {
+    CHECK(check_ptr(q, "q"));
+    CHECK(check_ptr(r, "r"));
+    return blas1(L, OP_SUB3, p, q, r, 0, 0, nullptr, flags, stream);
+}
+int nkv_axpy_dev(const nkv_layout* L, double* x, const double* alpha_dev, double sign,
+                 const double* y, unsigned flags, void* stream) {
+    CHECK(check_ptr(y, "y"));
+    if (!alpha_dev) return fail(NKV_EINVAL, "alpha_dev is NULL");
+    return blas1(L, OP_AXPY_DEV, x, y, nullptr, 0, sign, alpha_dev, flags, stream);
+}
+
+int nkv_normalize_dev(const nkv_layout* L, double* x, const double* nrm2_dev, double* beta_dev,
+                      unsigned flags, void* stream) {
+    (void)flags;
+    CHECK(check_layout(L));
+    CHECK(check_ptr(x, "x"));
+    if (!nrm2_dev) return fail(NKV_EINVAL, "nrm2_dev is NULL");
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), x, nrm2_dev,
+                       x, rows, rows, 0, nullptr, nullptr, nullptr, beta_dev);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_dot(const nkv_layout* L, const double* w, const double* a, const double* b, double* out_dev,
+            void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(a, "a"));
+    CHECK(check_ptr(b, "b"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!out_dev) return fail(NKV_EINVAL, "out_dev is NULL");
+    return launch_block_dot(L, w, a, L->ld, 1, b, out_dev, ws, flags, S(stream));
+}
+
+int nkv_block_dot(const nkv_layout* L, const double* w, const double* Q, int j, const double* f,
+                  double* h_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
+    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    return launch_block_dot(L, w, Q, L->ld, j, f, h_dev, ws, flags, S(stream));
+}
+
+int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
+                     double* f, double* nrm2_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
+    if (j < 0) return fail(NKV_EINVAL, "j=%d < 0", j);
+    const bool over = (flags & NKV_OVERWRITE) != 0;
+    const bool norm = (flags & NKV_NORM2) != 0;
+    if (norm) {
+        CHECK(check_ptr(w, "w"));
+        CHECK(check_ptr(ws, "ws"));
+        if (!nrm2_dev) return fail(NKV_EINVAL, "nrm2_dev is NULL");
+    }
+    const int tpf = (int)(L->sv / kTile);
+    const int tiles_w = tpf * L->n_wf;
+    const int tiles_total = (int)(rows_of(L) / kTile);
+    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    if (g < 1) g = 1;
+    const int64_t T = rows_of(L);
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    double* part = ws ? partials_of(ws) : nullptr;
+    hipStream_t st = S(stream);
+    if (over && norm)
+        hipLaunchKernelGGL((k_block_update<true, true>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else if (over)
+        hipLaunchKernelGGL((k_block_update<true, false>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else if (norm)
+        hipLaunchKernelGGL((k_block_update<false, true>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else
+        hipLaunchKernelGGL((k_block_update<false, false>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    NKV_LAUNCHED();
+    if (norm) {
+        // ||f||^2 time term: (uparam(1)==2.1 / real_dot) only on the rank owning the replicated scalar
+        const bool tdot = (flags & NKV_TIME) && L->rank0;
+        hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev,
+                           tdot ? f + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nan_flag_of(ws));
+        NKV_LAUNCHED();
+    }
+    return NKV_OK;
+}
+
+int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,
+                       int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
+                       unsigned flags, void* stream) {
+    (void)flags;
+    CHECK(check_layout(L));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(q_out, "q_out"));
+    if (!nrm2_dev) return fail(NKV_EINVAL, "nrm2_dev is NULL");
+    if (hcol_dev && (!h1_dev || j < 0)) return fail(NKV_EINVAL, "hcol needs h1 and j >= 0");
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), f, nrm2_dev,
+                       q_out, rows, rows, j, h1_dev, h2_dev, hcol_dev, nullptr);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    if (!V_dev) return fail(NKV_EINVAL, "V_dev is NULL");
+    if (k < 1 || k > kRotMaxK) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d]", k, kRotMaxK);
+    if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
+    const size_t lds = ((size_t)k * kRotRows + 16 * 64) * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NKV_HIP(hipFuncSetAttribute((const void*)k_rotate, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(((size_t)kRotMaxK * kRotRows + 16 * 64) * sizeof(double))));
+        attr_set = true;
+    }
+    const int64_t n_tiles = rows_of(L) / kRotRows;
+    int64_t g = n_tiles < 4096 ? n_tiles : 4096;
+    if (g < 1) return NKV_OK;
+    hipLaunchKernelGGL(k_rotate, dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k, V_dev,
+                       ldv, n_tiles);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y, double time_scale,
+                void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(d, "d"));
+    CHECK(check_ptr(x, "x"));
+    CHECK(check_ptr(y, "y"));
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_op_diag, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), d, x, y, rows,
+                       rows, time_scale);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_op_rot2(const nkv_layout* L, const double* c, const double* s, const double* d_rest,
+                const double* x, double* y, int transpose, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(c, "c"));
+    CHECK(check_ptr(s, "s"));
+    CHECK(check_ptr(x, "x"));
+    CHECK(check_ptr(y, "y"));
+    if (d_rest) CHECK(check_ptr(d_rest, "d_rest"));
+    if (L->n_wf < 2) return fail(NKV_EINVAL, "rot2 needs two velocity fields");
+    if (x == y) return fail(NKV_EINVAL, "rot2 cannot run in place");
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_op_rot2, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), c, s, d_rest, x,
+                       y, L->sv, rows, rows, transpose ? -1.0 : 1.0);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_fill_hash(const nkv_layout* L, double* x, uint64_t seed, int64_t v_offset, int64_t p_offset,
+                  void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(x, "x"));
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_fill_hash, dim3(grid_for(rows)), dim3(kThreads), 0, S(stream), x, seed, L->n_wf,
+                       L->n_v, L->sv, L->n_p, rows, rows, v_offset, p_offset);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+"""Krylov–Schur eigensolver driver (host control flow, device basis).
+
+Reference: ``krylov_schur`` (core/eigensolvers.f90:120-359) and ``schur_condensation`` (:363-468).
+Control flow restated one-for-one:
+
+    repeat
+        arnoldi_factorization(Q, H, mstart, k_dim)                          :298
+        vals, vecs = eig(H(1:k,1:k))          (dgeev, sorted by |lambda|)      :306
+        residual = |H(k+1,k) * vecs(k,:)|;  cnt = #(residual < eigen_tol)      :309-310
+        stop if schur_tgt <= 0 or cnt >= schur_tgt, else schur_condensation    :314-331
+    until converged
+
+``schur_condensation``: b = H(k+1,k) e_k; (T, Z) = dgees(H_k) sorted |lambda|>0.9; select
+(|lambda| >= 1-schur_del) U (nev+4 largest); dtrsen; zero the unwanted blocks; Q(:,1:k) <- Q(:,1:k) Z
+(device, in place — the reference copies the whole basis twice, :421-432); H(ms+1,:) = b^T Z;
+mstart = ms+1; Q(mstart) <- Q(k+1).
+
+The dense k x k work runs on the host (lapack.py), identically on every rank.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import lapack
+from .arnoldi import HessenbergDev, arnoldi_factorization
+from .config import KrylovSchurConfig
+from .operators import LinearOperator
+from .vector import Basis, NekContext, NekVector
+
+
+@dataclass
+class KrylovSchurResult:
+    vals: np.ndarray            # Ritz values of H_k, sorted by decreasing modulus (complex)
+    vecs: np.ndarray            # corresponding eigenvectors of H_k (k x k complex)
+    residual: np.ndarray        # |H(k+1,k) vecs(k,:)| (Ritz residual estimates)
+    converged: int              # count(residual < eigen_tol)
+    schur_cnt: int              # number of Schur condensations (restarts)
+    H: np.ndarray               # final (k+1) x k Hessenberg/Krylov–Schur matrix
+    Q: Basis                    # the resident basis (k+1 vectors)
+    mstart_history: list = field(default_factory=list)   # mstart after each condensation
+    cnt_history: list = field(default_factory=list)      # converged count after each factorisation
+    selected_history: list = field(default_factory=list)  # selected masks per condensation
+
+
+def prepare_seed(seed: NekVector, Q0: NekVector) -> float:
+    """X(1) = seed / sqrt(<seed, seed>) with real_dot (incl. time) — core/linear_stab.f90:287-291."""
+    Q0.copy_from(seed)
+    alpha = float(np.sqrt(Q0.dot(Q0)))
+    Q0.scal(1.0 / alpha)
+    return alpha
+
+
+def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: KrylovSchurConfig):
+    """One Krylov–Schur restart.  Mutates H (host) and Q (device); returns (mstart, selected)."""
+    b_vec = np.zeros(k)
+    b_vec[k - 1] = H[k, k - 1]
+    T, Z, vals = lapack.schur(H[:k, :k])
+    selected, ms = lapack.select_eigenvalues(vals, cfg.schur_del, cfg.schur_tgt, faithful=cfg.faithful_select)
+    T, Z, _m = lapack.ordschur(T, Z, selected)
+    H[:k, :k] = T
+    H[:ms, ms:k] = 0.0
+    H[ms:k + 1, :] = 0.0
+    Zd = torch.as_tensor(np.asfortranarray(Z).ravel(order="F")).to(ctx.device)
+    ctx.call("nkv_rotate", Q.ptr, int(k), Zd.data_ptr(), int(k), ctx.stream)
+    H[ms, :] = b_vec @ Z
+    mstart = ms + 1
+    # Q(mstart) <- Q(k+1): nopcopy moves the fields only, not time (:458-459)
+    Q[mstart - 1].copy_from(Q[k], time=False)
+    return mstart, selected
+
+
+def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: KrylovSchurConfig | None = None,
+                 transpose: bool = False, on_restart=None) -> KrylovSchurResult:
+    """Eigenpairs of ``op`` of largest modulus by Krylov–Schur restarts (reference defaults from
+    core/main.f90:9-12: k_dim=100, schur_tgt=2, eigen_tol=1e-6, schur_del=0.1)."""
+    cfg = cfg or KrylovSchurConfig()
+    k = cfg.k_dim
+    Q = ctx.basis(k + 1)
+    Hd = HessenbergDev(ctx, k)
+    H = np.zeros((k + 1, k), order="F")
+    f = ctx.vector()
+    if cfg.seed_mode == "normalize":
+        prepare_seed(seed, Q[0])
+    elif cfg.seed_mode == "noise":
+        # ifseed_nois branch of the in-tree driver: Q(1) = A (seed/||seed||), NOT renormalised
+        # (eigensolvers.f90:195-203)
+        w2 = ctx.vector()
+        w2.copy_from(seed)
+        from .vector import k_normalize
+        k_normalize(w2)
+        (op.rmatvec if transpose else op.matvec)(w2, Q[0])
+    elif cfg.seed_mode == "as_is":
+        Q[0].copy_from(seed)
+    else:
+        raise ValueError(cfg.seed_mode)
+
+    mstart = 1
+    schur_cnt = 0
+    res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
+    while True:
+        arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose)
+        H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
+        ctx.check_nan()
+        vals, vecs = lapack.eig(H[:k, :k])
+        residual = np.abs(H[k, k - 1] * vecs[k - 1, :])
+        cnt = int(np.count_nonzero(residual < cfg.eigen_tol))
+        res.cnt_history.append(cnt)
+        if cfg.schur_tgt <= 0 or cnt >= cfg.schur_tgt or schur_cnt >= cfg.max_restarts:
+            break
+        schur_cnt += 1
+        mstart, selected = schur_condensation(ctx, H, Q, k, cfg)
+        res.mstart_history.append(mstart)
+        res.selected_history.append(selected)
+        Hd.upload(H)
+        if on_restart is not None:
+            on_restart(schur_cnt, mstart)
+    res.vals, res.vecs, res.residual, res.converged, res.schur_cnt = vals, vecs, residual, cnt, schur_cnt
+    res.H = H
+    return res
+
+
+def ritz_vector(ctx: NekContext, Q: Basis, vecs: np.ndarray, i: int, out_re: NekVector, out_im: NekVector,
+                k: int | None = None) -> tuple[float, float]:
+    """Eigenmode i from the basis: fp = Q(:,1:k) vecs(:,i) (complex, as two real combinations),
+    normalised so that ||Re||^2 + ||Im||^2 = 1 (outpost_ks, eigensolvers.f90:565-585, 603-613).
+    Returns (||Re||, ||Im||) before normalisation."""
+    from .vector import combine
+
+    k = vecs.shape[0] if k is None else k
+    yr = torch.as_tensor(np.ascontiguousarray(vecs[:k, i].real)).to(ctx.device)
+    yi = torch.as_tensor(np.ascontiguousarray(vecs[:k, i].imag)).to(ctx.device)
+    combine(out_re, Q, yr, k, with_time=False)
+    combine(out_im, Q, yi, k, with_time=False)
+    a_r = float(np.sqrt(ctx.dot(out_re, out_re, time=False)))
+    a_i = float(np.sqrt(ctx.dot(out_im, out_im, time=False)))
+    beta = 1.0 / np.sqrt(a_r ** 2 + a_i ** 2)
+    out_re.scal(beta)
+    out_im.scal(beta)
+    return a_r, a_i

@@ -1,0 +1,137 @@
+"""Linear operators: the matvec boundary of the Krylov path.
+
+Reference: LightKrylov ``abstract_linop`` extended by ``exponential_prop`` with type-bound
+``matvec(self, vec_in, vec_out)`` / ``rmatvec`` (core/linear_operators.f90:17-23, 39-103) and the
+legacy ``matvec(f, q)`` dispatcher (core/matvec.f90:56-146).  In nekStab the operator body is a
+Nek5000 time integration (out of scope here); the operators below are the synthetic, exactly
+known ones SURVEY.md §8(d) defines for every BASELINE config, each a device kernel or a
+composition of the library's device ops.  Any Python object with ``matvec(x, y)`` (and optionally
+``rmatvec``) over :class:`~nekstab_next_amd.vector.NekVector` plugs into the solvers.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .vector import NekContext, NekVector
+
+
+class LinearOperator:
+    """y <- A x (matvec) and y <- A^T x under the W inner product (rmatvec)."""
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def rmatvec(self, x: NekVector, y: NekVector) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+def _dev(ctx: NekContext, a: np.ndarray) -> torch.Tensor:
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(ctx.device)
+
+
+class DiagOperator(LinearOperator):
+    """y = D x with D diagonal over every stored row (self-adjoint under W).
+
+    ``diag`` is a padded host/device vector of length ``layout.ld`` (this rank's shard); padding
+    rows are ignored.  ``time_scale`` multiplies the scalar time component.
+    """
+
+    def __init__(self, ctx: NekContext, diag, time_scale: float = 0.0):
+        self.ctx = ctx
+        d = diag if isinstance(diag, torch.Tensor) else _dev(ctx, diag)
+        if d.numel() != ctx.layout.ld:
+            raise ValueError("diag must have layout.ld entries")
+        self.d = d.to(ctx.device, torch.float64).contiguous()
+        self.time_scale = float(time_scale)
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:
+        self.ctx.call("nkv_op_diag", self.d.data_ptr(), x.ptr, y.ptr, self.time_scale, self.ctx.stream)
+
+    rmatvec = matvec
+
+
+class Rot2Operator(LinearOperator):
+    """Per grid point, (vx, vy) -> r R(theta) (vx, vy); other weighted fields and pressure are
+    multiplied by ``d_rest``.  W-normal (the 2x2 blocks share one weight), eigenvalues
+    r e^{±i theta}: conjugate pairs for the complex handling of ``eig`` / ``select_eigenvalues``
+    (SURVEY.md §8(d) config 2).  ``rmatvec`` applies r R(-theta)."""
+
+    def __init__(self, ctx: NekContext, c, s, d_rest=None):
+        self.ctx = ctx
+        lay = ctx.layout
+        self.c = c if isinstance(c, torch.Tensor) else _dev(ctx, c)
+        self.s = s if isinstance(s, torch.Tensor) else _dev(ctx, s)
+        if self.c.numel() != lay.sv or self.s.numel() != lay.sv:
+            raise ValueError("c, s must have layout.sv entries")
+        self.d_rest = None
+        if d_rest is not None:
+            self.d_rest = d_rest if isinstance(d_rest, torch.Tensor) else _dev(ctx, d_rest)
+            if self.d_rest.numel() != lay.ld:
+                raise ValueError("d_rest must have layout.ld entries")
+
+    def _apply(self, x, y, transpose):
+        dr = self.d_rest.data_ptr() if self.d_rest is not None else None
+        self.ctx.call("nkv_op_rot2", self.c.data_ptr(), self.s.data_ptr(), dr, x.ptr, y.ptr, int(transpose),
+                      self.ctx.stream)
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:
+        self._apply(x, y, False)
+
+    def rmatvec(self, x: NekVector, y: NekVector) -> None:
+        self._apply(x, y, True)
+
+
+class ShiftedOperator(LinearOperator):
+    """y = A x + shift * x  (e.g. the Newton–Krylov Jacobian-minus-identity J = D - I, config 4;
+    the reference's newton_linearized_map returns Phi'(q) - q, core/matvec.f90:520-571)."""
+
+    def __init__(self, base: LinearOperator, shift: float):
+        self.base, self.shift = base, float(shift)
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:
+        self.base.matvec(x, y)
+        y.axpby(1.0, x, self.shift)
+
+    def rmatvec(self, x: NekVector, y: NekVector) -> None:
+        self.base.rmatvec(x, y)
+        y.axpby(1.0, x, self.shift)
+
+
+class RankTwoPerturbed(LinearOperator):
+    """A x = D x + sigma * (u <v, x>_W + v' <u', x>_W): a diagonal plus a rank-2 non-normal term,
+    so direct and adjoint eigenvectors differ.  The adjoint under W is
+    A^T x = D x + sigma * (v <u, x>_W + u' <v', x>_W)."""
+
+    def __init__(self, diag_op: DiagOperator, u: NekVector, v: NekVector, u2: NekVector, v2: NekVector,
+                 sigma: float):
+        self.d, self.u, self.v, self.u2, self.v2, self.sigma = diag_op, u, v, u2, v2, float(sigma)
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:
+        self.d.matvec(x, y)
+        a = x.ctx.dot(self.v, x, time=False)
+        b = x.ctx.dot(self.u2, x, time=False)
+        y.axpby(1.0, self.u, self.sigma * a)
+        y.axpby(1.0, self.v2, self.sigma * b)
+
+    def rmatvec(self, x: NekVector, y: NekVector) -> None:
+        self.d.matvec(x, y)
+        a = x.ctx.dot(self.u, x, time=False)
+        b = x.ctx.dot(self.v2, x, time=False)
+        y.axpby(1.0, self.v, self.sigma * a)
+        y.axpby(1.0, self.u2, self.sigma * b)
+
+
+class CallableOperator(LinearOperator):
+    """Wrap plain callables ``f(x, y)`` (e.g. a user's time-stepper driving the GPU state)."""
+
+    def __init__(self, matvec, rmatvec=None):
+        self._mv, self._rmv = matvec, rmatvec
+
+    def matvec(self, x, y):
+        self._mv(x, y)
+
+    def rmatvec(self, x, y):
+        if self._rmv is None:
+            raise NotImplementedError("operator has no adjoint")
+        self._rmv(x, y)

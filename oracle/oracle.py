@@ -1,0 +1,354 @@
+"""CPU oracle for nekStab's Krylov hot path.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker / the timed CPU baseline.  The product (``nekstab_next_amd``)
+never imports it.
+
+What it restates (each function cites the reference line it follows):
+* vector algebra, ``update_hessenberg_matrix`` (MGS2), ``k_matmul``, the restart rotation, the
+  ordering rules ``quicksort2`` / ``select_eigenvalues`` / ``sort_eigendecomp``: plain C in
+  ``nekstab_oracle.c`` (reference operation order, no FP contraction);
+* the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
+  ``ts_gmres``, ``biorthogonalize``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
+  dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
+
+Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
+golden vectors for this path, and its Fortran cannot be built here without
+writing stand-ins for Nek5000's SIZE/TOTAL include files and routines (glsc3, rzero, ...), which
+this build does not do.  The restatement is pinned instead to closed-form known answers
+(synthetic operators with exact spectra / exact solutions, tests/test_oracle_known_answers.py)
+and to fixtures it generated (tests/golden/).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_double, c_int, c_int32, c_int64, c_uint64
+
+import numpy as np
+from scipy.linalg import lapack as _lp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+
+class orc_layout(Structure):
+    _fields_ = [("nv", c_int64), ("np", c_int64), ("nwf", c_int32), ("time_in_dot", c_int32)]
+
+
+_D = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_LP = POINTER(orc_layout)
+
+_SIGS = {
+    "orc_set_threads": (None, [c_int]),
+    "orc_max_threads": (c_int, []),
+    "orc_vector_len": (c_int64, [_LP]),
+    "orc_glsc3": (c_double, [_D, _D, _D, c_int64]),
+    "orc_k_dot": (c_double, [_LP, _D, _D, _D]),
+    "orc_real_dot": (c_double, [_LP, _D, _D, _D]),
+    "orc_k_cmult": (None, [_LP, _D, c_double]),
+    "orc_k_add2": (None, [_LP, _D, _D]),
+    "orc_k_sub2": (None, [_LP, _D, _D]),
+    "orc_k_sub3": (None, [_LP, _D, _D, _D]),
+    "orc_k_zero": (None, [_LP, _D]),
+    "orc_k_copy": (None, [_LP, _D, _D]),
+    "orc_real_axpby": (None, [_LP, _D, c_double, _D, c_double]),
+    "orc_update_hessenberg": (None, [_LP, _D, _D, _D, _D, c_int, _D]),
+    "orc_k_matmul": (None, [_LP, _D, _D, _D, c_int]),
+    "orc_rotate": (None, [_LP, _D, c_int, _D]),
+    "orc_op_diag": (None, [_LP, _D, _D, _D, c_double]),
+    "orc_fill_hash": (None, [_LP, _D, c_uint64, c_int64, c_int64]),
+    "orc_quicksort2": (None, [c_int, _D, _I]),
+    "orc_select_eigenvalues": (c_int, [c_int, _D, _D, c_double, c_int, _I]),
+    "orc_sort_eigendecomp": (None, [c_int, _D, _D, _D, _D]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        L = ctypes.CDLL(_LIB_PATH)
+        for k, (r, a) in _SIGS.items():
+            f = getattr(L, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(int(n))
+
+
+class OLayout:
+    """Unpadded reference layout [vx | vy | (vz) | t.. | pr | time] of one shard."""
+
+    def __init__(self, nv: int, np_: int, nwf: int, time_in_dot: bool = False, ldim: int | None = None):
+        self.c = orc_layout(nv, np_, nwf, int(time_in_dot))
+        self.nv, self.np, self.nwf = nv, np_, nwf
+        self.ldim = ldim if ldim is not None else min(nwf, 3)
+        self.n = nwf * nv + np_
+        self.len = self.n + 1
+
+    @classmethod
+    def from_nek(cls, ldim, lx1, lx2, nelv, n_scalars=0, ifpo=True, time_in_dot=False):
+        return cls(lx1 ** ldim * nelv, (lx2 ** ldim * nelv) if ifpo else 0, ldim + n_scalars, time_in_dot, ldim)
+
+    def zeros(self, k=None):
+        return np.zeros(self.len if k is None else (k, self.len))
+
+
+# ---- vector ops ---------------------------------------------------------------------------------
+
+def k_dot(L: OLayout, w, p, q) -> float:
+    return lib().orc_k_dot(ctypes.byref(L.c), w, p, q)
+
+
+def real_dot(L: OLayout, w, p, q) -> float:
+    return lib().orc_real_dot(ctypes.byref(L.c), w, p, q)
+
+
+def k_normalize(L: OLayout, w, p) -> float:
+    a = float(np.sqrt(k_dot(L, w, p, p)))
+    lib().orc_k_cmult(ctypes.byref(L.c), p, 1.0 / a)
+    return a
+
+
+def fill_hash(L: OLayout, seed: int, voff: int = 0, poff: int = 0) -> np.ndarray:
+    x = L.zeros()
+    lib().orc_fill_hash(ctypes.byref(L.c), x, int(seed) & (2**64 - 1), int(voff), int(poff))
+    return x
+
+
+def fill_hash_np(nwf, nv, np_, seed, voff=0, poff=0) -> np.ndarray:
+    """Pure-numpy twin of orc_fill_hash (vectorised uint64 arithmetic)."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def mix(z):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        key0 = np.uint64((int(seed) * 0xD1342543DE82EF95) & int(M))
+        out = []
+        for f in range(nwf):
+            g = np.arange(voff, voff + nv, dtype=np.uint64)
+            z = mix(key0 + np.uint64((f * 0x9E3779B97F4A7C15) & int(M)) + g)
+            out.append(2.0 * ((z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53) - 1.0)
+        g = np.arange(poff, poff + np_, dtype=np.uint64)
+        z = mix(key0 + np.uint64((31 * 0x9E3779B97F4A7C15) & int(M)) + g)
+        out.append(2.0 * ((z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53) - 1.0)
+    return np.concatenate(out + [np.zeros(1)])
+
+
+# ---- ordering rules (C transliteration) ---------------------------------------------------------
+
+def quicksort2(arr):
+    a = np.ascontiguousarray(arr, dtype=np.float64).copy()
+    idx = np.arange(1, a.size + 1, dtype=np.int32)
+    lib().orc_quicksort2(a.size, a, idx)
+    return idx - 1, a
+
+
+def select_eigenvalues(vals, delta, nev):
+    re = np.ascontiguousarray(vals.real, dtype=np.float64)
+    im = np.ascontiguousarray(vals.imag, dtype=np.float64)
+    sel = np.zeros(vals.size, dtype=np.int32)
+    cnt = lib().orc_select_eigenvalues(vals.size, re, im, float(delta), int(nev), sel)
+    return sel.astype(bool), int(cnt)
+
+
+def sort_eigendecomp(vals, vecs):
+    n = vals.size
+    re, im = vals.real.copy(), vals.imag.copy()
+    vre = np.ascontiguousarray(vecs.real.T).copy()  # column-major -> rows are columns
+    vim = np.ascontiguousarray(vecs.imag.T).copy()
+    lib().orc_sort_eigendecomp(n, re, im, vre, vim)
+    return re + 1j * im, (vre + 1j * vim).T
+
+
+# ---- dense steps (lapack_wrapper.f90) -----------------------------------------------------------
+
+def eig(A):
+    """lapack_wrapper.f90:114-177: dgeev('N','V', lwork=4n) on a copy, conjugate-pair assembly,
+    sort_eigendecomp."""
+    n = A.shape[0]
+    wr, wi, _, vr, info = _lp.dgeev(np.array(A, order="F", copy=True), compute_vl=0, compute_vr=1, lwork=4 * n)
+    assert info == 0, info
+    vecs = np.array(vr, dtype=np.complex128)
+    i = 0
+    while i < n - 1:  # do i = 1, n-1 with the same two branches
+        if wi[i] > 0:
+            vecs[:, i] = vr[:, i] + 1j * vr[:, i + 1]
+            vecs[:, i + 1] = vr[:, i] - 1j * vr[:, i + 1]
+        elif wi[i] == 0:
+            vecs[:, i] = vr[:, i]
+        i += 1
+    return sort_eigendecomp(wr + 1j * wi, vecs)
+
+
+def schur_sorted(A):
+    """lapack_wrapper.f90:3-55: dgees('V','S', select_eigvals: sqrt(wr**2+wi**2) > 0.9, lwork=3n)."""
+    n = A.shape[0]
+    t, _, wr, wi, vs, _, info = _lp.dgees(lambda a, b: int(np.sqrt(a ** 2 + b ** 2) > 0.9),
+                                          np.array(A, order="F", copy=True), compute_v=1, sort_t=1, lwork=3 * n)
+    return np.array(t, order="F"), np.array(vs, order="F"), wr + 1j * wi
+
+
+def ordschur(T, Z, selected):
+    """lapack_wrapper.f90:59-111: dtrsen('N','V'), lwork=n, liwork=1."""
+    n = T.shape[0]
+    ts, qs, _, _, m, _, _, info = _lp.dtrsen(selected.astype(np.int32), T, Z, job="N", wantq=1, lwork=n, liwork=1)
+    assert info == 0, info
+    return np.array(ts, order="F"), np.array(qs, order="F")
+
+
+def lstsq(A, b):
+    """lapack_wrapper.f90:248-300: dgels('N'), lwork=2mn; x = b_tilde(1:n)."""
+    m, n = A.shape
+    _, x, info = _lp.dgels(np.array(A, order="F", copy=True), np.array(b, copy=True), trans="N", lwork=2 * m * n)
+    return np.array(x[:n])
+
+
+# ---- drivers ------------------------------------------------------------------------------------
+
+def arnoldi_factorization(L: OLayout, w, matvec, Q, H, mstart, mend):
+    """krylov_decomposition.f90:2-99 with update_hessenberg_matrix in C.  Q: (k+1, L.len) array;
+    H: (k+1, k) array, columns written in place (1-based mstart..mend)."""
+    f = L.zeros()
+    wrk = L.zeros()
+    for mstep in range(mstart, mend + 1):
+        matvec(Q[mstep - 1], f)
+        col = np.zeros(mstep + 1)
+        lib().orc_update_hessenberg(ctypes.byref(L.c), w, col, f, np.ascontiguousarray(Q[:mstep]), mstep, wrk)
+        H[: mstep + 1, mstep - 1] = col
+        Q[mstep] = f
+
+
+def schur_condensation(L: OLayout, H, Q, k, schur_del, schur_tgt):
+    """eigensolvers.f90:363-468.  Returns (mstart, selected)."""
+    b_vec = np.zeros(k)
+    b_vec[k - 1] = H[k, k - 1]
+    T, vecs, vals = schur_sorted(H[:k, :k])
+    selected, ms = select_eigenvalues(vals, schur_del, schur_tgt)
+    T, vecs = ordschur(T, vecs, selected)
+    H[:k, :k] = T
+    H[:ms, ms:k] = 0.0
+    H[ms:k + 1, :] = 0.0
+    Qk = np.ascontiguousarray(Q[:k])
+    lib().orc_rotate(ctypes.byref(L.c), Qk, k, np.ascontiguousarray(vecs.ravel(order="F")))
+    Q[:k, :L.n] = Qk[:, :L.n]
+    H[ms, :] = b_vec @ vecs
+    mstart = ms + 1
+    Q[mstart - 1, :L.n] = Q[k, :L.n]  # nopcopy: fields only
+    return mstart, selected
+
+
+def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, schur_del=0.1, max_restarts=1000):
+    """eigensolvers.f90:120-359 from a given first Krylov vector q1 (already normalised by the
+    caller as prepare_seed does, linear_stab.f90:287-291)."""
+    Q = np.zeros((k_dim + 1, L.len))
+    H = np.zeros((k_dim + 1, k_dim))
+    Q[0] = q1
+    mstart, schur_cnt = 1, 0
+    hist = dict(mstart=[], cnt=[], selected=[], H_first=None)
+    while True:
+        arnoldi_factorization(L, w, matvec, Q, H, mstart, k_dim)
+        if hist["H_first"] is None:
+            hist["H_first"] = H.copy()
+        vals, vecs = eig(H[:k_dim, :k_dim])
+        residual = np.abs(H[k_dim, k_dim - 1] * vecs[k_dim - 1, :])
+        cnt = int(np.count_nonzero(residual < eigen_tol))
+        hist["cnt"].append(cnt)
+        if schur_tgt <= 0 or cnt >= schur_tgt or schur_cnt >= max_restarts:
+            break
+        schur_cnt += 1
+        mstart, sel = schur_condensation(L, H, Q, k_dim, schur_del, schur_tgt)
+        hist["mstart"].append(mstart)
+        hist["selected"].append(sel)
+    return dict(vals=vals, vecs=vecs, residual=residual, converged=cnt, schur_cnt=schur_cnt, H=H, Q=Q, **hist)
+
+
+def prepare_seed(L: OLayout, w, seed):
+    """linear_stab.f90:287-291: X(1) = seed / sqrt(real_dot(seed, seed))."""
+    x = seed.copy()
+    a = np.sqrt(real_dot(L, w, x, x))
+    lib().orc_k_cmult(ctypes.byref(L.c), x, 1.0 / a)
+    return x
+
+
+def ts_gmres(L: OLayout, w, matvec, rhs, maxiter, ksize, tol, findiff=False):
+    """newton_krylov.f90:170-299 (+ initialize_gmres_vector :303-326).  Returns (sol, history)."""
+    c = ctypes.byref(L.c)
+    Q = np.zeros((ksize + 1, L.len))
+    sol = L.zeros()
+    Q[0] = rhs
+    beta = k_normalize(L, w, Q[0])
+    hist = dict(inner=[], outer=[], y=[])
+    for _it in range(maxiter):
+        H = np.zeros((ksize + 1, ksize))
+        yvec = np.zeros(ksize)
+        evec = np.zeros(ksize + 1)
+        evec[0] = beta
+        Q[1:] = 0.0
+        k_used = ksize
+        for k in range(1, ksize + 1):
+            arnoldi_factorization(L, w, matvec, Q, H, k, k)
+            yvec[:k] = lstsq(H[: k + 1, :k], evec[: k + 1])
+            beta = float(np.linalg.norm(evec[: k + 1] - H[: k + 1, :k] @ yvec[:k]))
+            hist["inner"].append(beta ** 2)
+            k_used = k
+            if beta ** 2 < tol or (findiff and beta ** 2 < 1e-8):
+                break
+        hist["y"].append(yvec[:k_used].copy())
+        dq = L.zeros()
+        lib().orc_k_matmul(c, dq, np.ascontiguousarray(Q[:k_used]), np.ascontiguousarray(yvec[:k_used]), k_used)
+        lib().orc_k_add2(c, sol, dq)
+        # initialize_gmres_vector(beta, Q(1)=sol, rhs): f = -(A sol - rhs); normalise
+        Q[0] = sol
+        f = L.zeros()
+        matvec(Q[0], f)
+        lib().orc_k_sub2(c, f, rhs)
+        lib().orc_k_cmult(c, f, -1.0)
+        beta = k_normalize(L, w, f)
+        Q[0] = f
+        hist["outer"].append(beta ** 2)
+        if beta ** 2 < tol or (findiff and beta ** 2 < 1e-6):
+            break
+    return sol, hist
+
+
+def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):
+    """sensitivity.f90:393-469.  Inputs are modified copies; returns (dRe, dIm, aRe, aIm).
+
+    The direct mode is normalised with opcmult (velocities only, not pressure/scalars, :429-430);
+    inner products use the weighted fields (inner_product, eigensolvers.f90:3-56)."""
+    dRe, dIm, aRe, aIm = (x.copy() for x in (dRe, dIm, aRe, aIm))
+    ip = lambda p, q: k_dot(OLayout(L.nv, L.np, L.nwf, False, L.ldim), w, p, q)  # noqa: E731
+    alpha = ip(dRe, dRe)
+    beta = ip(dIm, dIm)
+    gamma = 1.0 / np.sqrt(alpha + beta)
+    nvel = L.ldim * L.nv
+    dRe[:nvel] *= gamma
+    dIm[:nvel] *= gamma
+    alpha = ip(aRe, dRe)
+    beta = ip(aIm, dIm)
+    gamma = alpha + beta
+    alpha = ip(aRe, dIm)
+    beta = ip(aIm, dRe)
+    delta = alpha - beta
+    den = gamma ** 2 + delta ** 2
+    n = L.n
+    r = (gamma * aRe[:n] - delta * aIm[:n]) / den
+    i = (gamma * aIm[:n] + delta * aRe[:n]) / den
+    aRe[:n], aIm[:n] = r, i
+    return dRe, dIm, aRe, aIm

@@ -1,0 +1,273 @@
+"""GPU parity of every C-ABI entry point against the CPU oracle / numpy on the same inputs.
+
+Tolerances: data movement (zero/copy/fill/rotate of exact values) is bit-exact; BLAS-1 updates
+agree to 1 ulp-level (the device contracts a*x+b*y into one FMA, the oracle does not); reductions
+are regrouped (tree vs sequential), so dots agree to 1e-13 relative.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as orc
+from helpers import olayout
+from nekstab_next_amd import synthetic as syn
+from nekstab_next_amd._lib import NKV_NORM2, NKV_OVERWRITE, NKV_TIME, NkvNaNError
+from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
+from nekstab_next_amd.layout import NekLayout
+from nekstab_next_amd.operators import DiagOperator, Rot2Operator
+from nekstab_next_amd.vector import NekContext, k_matmul, k_normalize
+
+pytestmark = pytest.mark.gpu
+
+LAYOUTS = {
+    "2d": NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300),
+    "3d_scalar": NekLayout(ldim=3, lx1=5, lx2=3, nelgv=37, n_scalars=1),  # odd sizes, ragged pads
+}
+
+
+def make_ctx(lay, weights=None, **kw):
+    w = syn.mass_weights(lay) if weights is None else weights
+    return NekContext(lay, weights=w, **kw), w
+
+
+def dev_vec(ctx, padded):
+    return ctx.vector().from_packed(padded)
+
+
+@pytest.mark.parametrize("name", list(LAYOUTS))
+def test_fill_hash_bitexact(gpu, name):
+    lay = LAYOUTS[name]
+    ctx, _ = make_ctx(lay)
+    v = ctx.vector()
+    v.fill_hash(1234)
+    np.testing.assert_array_equal(v.to_packed(), syn.hash_vector(lay, 1234))
+    L = olayout(lay)
+    np.testing.assert_array_equal(syn.to_reference_order(lay, v.to_packed()), orc.fill_hash(L, 1234))
+
+
+@pytest.mark.parametrize("name", list(LAYOUTS))
+def test_blas1_vs_oracle(gpu, name):
+    lay = LAYOUTS[name]
+    ctx, w = make_ctx(lay)
+    L = olayout(lay)
+    c = ctypes.byref(L.c)
+    a = syn.hash_vector(lay, 1)
+    b = syn.hash_vector(lay, 2)
+    a[lay.time_offset], b[lay.time_offset] = 0.25, -1.5
+    ra, rb = syn.to_reference_order(lay, a), syn.to_reference_order(lay, b)
+    x, y = dev_vec(ctx, a), dev_vec(ctx, b)
+
+    # real_axpby: time untouched
+    x.axpby(0.7, y, -1.3)
+    ref = ra.copy()
+    orc.lib().orc_real_axpby(c, ref, 0.7, rb, -1.3)
+    got = syn.to_reference_order(lay, x.to_packed())
+    np.testing.assert_allclose(got, ref, rtol=0, atol=4e-16 * 3)
+    assert got[-1] == 0.25
+    ref = got.copy()  # continue from the device state: the remaining ops are exact elementwise
+    # k_cmult / real_scal incl. time
+    x.scal(-2.5)
+    orc.lib().orc_k_cmult(c, ref, -2.5)
+    np.testing.assert_array_equal(syn.to_reference_order(lay, x.to_packed()), ref)
+    # copy / zero
+    z = ctx.vector()
+    z.copy_from(x)
+    np.testing.assert_array_equal(z.to_packed(), x.to_packed())
+    z.zero()
+    assert not np.any(z.to_packed())
+    # sub3 with time (k_sub3)
+    from nekstab_next_amd.vector import k_sub3, k_add2, k_sub2
+    k_sub3(z, x, y)
+    r3 = L.zeros()
+    orc.lib().orc_k_sub3(c, r3, ref, rb)
+    np.testing.assert_array_equal(syn.to_reference_order(lay, z.to_packed()), r3)
+    k_add2(z, y)
+    orc.lib().orc_k_add2(c, r3, rb)
+    np.testing.assert_array_equal(syn.to_reference_order(lay, z.to_packed()), r3)
+    k_sub2(z, x)
+    orc.lib().orc_k_sub2(c, r3, ref)
+    np.testing.assert_array_equal(syn.to_reference_order(lay, z.to_packed()), r3)
+    # padding rows stay zero
+    p = z.to_packed()
+    for _, s, n in lay.field_slices():
+        pad_end = s + (lay.sv if _ != "pr" else lay.sp)
+        assert not np.any(p[s + n:pad_end])
+
+
+@pytest.mark.parametrize("name", list(LAYOUTS))
+@pytest.mark.parametrize("time_in_dot", [False, True])
+def test_dot_vs_oracle(gpu, name, time_in_dot):
+    lay = LAYOUTS[name]
+    w = syn.sponge(syn.mass_weights(lay))  # zero weights inside a sponge are allowed
+    ctx, _ = make_ctx(lay, weights=w, time_in_dot=time_in_dot)
+    L = olayout(lay, time_in_dot)
+    a, b = syn.hash_vector(lay, 3), syn.hash_vector(lay, 4)
+    a[lay.time_offset], b[lay.time_offset] = 0.5, 3.0
+    x, y = dev_vec(ctx, a), dev_vec(ctx, b)
+    from nekstab_next_amd.vector import k_dot
+    got = k_dot(x, y)
+    ref = orc.k_dot(L, w, syn.to_reference_order(lay, a), syn.to_reference_order(lay, b))
+    assert abs(got - ref) <= 1e-13 * max(1.0, abs(ref))
+    # real_dot always includes time
+    got2 = x.dot(y)
+    ref2 = orc.real_dot(L, w, syn.to_reference_order(lay, a), syn.to_reference_order(lay, b))
+    assert abs(got2 - ref2) <= 1e-13 * max(1.0, abs(ref2))
+    # k_normalize
+    alpha = k_normalize(x)
+    ra = syn.to_reference_order(lay, a)
+    alpha_ref = orc.k_normalize(L, w, ra)
+    assert abs(alpha - alpha_ref) <= 1e-13 * alpha_ref
+    np.testing.assert_allclose(syn.to_reference_order(lay, x.to_packed()), ra, rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.parametrize("j", [1, 3, 4, 5, 37, 128])
+def test_block_dot_update_vs_numpy(gpu, j):
+    lay = LAYOUTS["2d"]
+    ctx, w = make_ctx(lay, max_cols=128)
+    Q = ctx.basis(j + 1)
+    for i in range(j):
+        Q[i].fill_hash(100 + i)
+    f = ctx.vector()
+    f.fill_hash(99)
+    Qh = Q.storage.cpu().numpy()[:j]
+    fh = f.to_packed()
+    wfull = np.zeros(lay.ld)
+    for f_ in range(lay.n_wf):
+        wfull[f_ * lay.sv: f_ * lay.sv + lay.n_v] = w
+    h = ctx.h1[:j]
+    ctx.call("nkv_block_dot", ctx.w.data_ptr(), Q.ptr, j, f.ptr, h.data_ptr(), ctx.ws.data_ptr(), 0, ctx.stream)
+    href = Qh @ (wfull * fh)
+    np.testing.assert_allclose(h.cpu().numpy(), href, rtol=1e-12, atol=1e-12 * np.abs(href).max())
+    # f <- f - Q h, fused norm
+    nrm = ctx.scal[5:6]
+    ctx.call("nkv_block_update", ctx.w.data_ptr(), Q.ptr, j, h.data_ptr(), f.ptr, nrm.data_ptr(),
+             ctx.ws.data_ptr(), NKV_NORM2 | NKV_TIME, ctx.stream)
+    hh = h.cpu().numpy()
+    fref = fh - hh @ Qh
+    np.testing.assert_allclose(f.to_packed(), fref, rtol=1e-12, atol=1e-13)
+    nref = np.sum(wfull * fref * fref)
+    assert abs(nrm.item() - nref) <= 1e-12 * nref
+    # overwrite (k_matmul): out = Q y incl. time
+    out = ctx.vector()
+    Q[0].time = 2.0
+    k_matmul(out, Q, hh, j)
+    Qh = Q.storage.cpu().numpy()[:j]
+    np.testing.assert_allclose(out.to_packed(), hh @ Qh, rtol=1e-12, atol=1e-13)
+
+
+def test_k_matmul_vs_oracle(gpu):
+    lay = LAYOUTS["3d_scalar"]
+    ctx, w = make_ctx(lay)
+    L = olayout(lay)
+    k = 9
+    Q = ctx.basis(k)
+    Qref = np.zeros((k, L.len))
+    for i in range(k):
+        v = syn.hash_vector(lay, 50 + i)
+        v[lay.time_offset] = 0.1 * i
+        Q[i].from_packed(v)
+        Qref[i] = syn.to_reference_order(lay, v)
+    y = np.linspace(-1, 1, k)
+    out = ctx.vector()
+    k_matmul(out, Q, y, k)
+    ref = L.zeros()
+    orc.lib().orc_k_matmul(ctypes.byref(L.c), ref, Qref, y, k)
+    np.testing.assert_allclose(syn.to_reference_order(lay, out.to_packed()), ref, rtol=1e-13, atol=1e-14)
+
+
+@pytest.mark.parametrize("k", [1, 7, 16, 64, 100, 129, 256])
+def test_rotate_vs_oracle(gpu, k):
+    lay = LAYOUTS["2d"]
+    ctx, _ = make_ctx(lay)
+    L = olayout(lay)
+    Q = ctx.basis(k + 1)
+    Qref = np.zeros((k + 1, L.len))
+    for i in range(k + 1):
+        v = syn.hash_vector(lay, 7 + i)
+        v[lay.time_offset] = 1.0 + i
+        Q[i].from_packed(v)
+        Qref[i] = syn.to_reference_order(lay, v)
+    V = np.linalg.qr(np.random.default_rng(k).standard_normal((k, k)))[0]
+    Vd = torch.as_tensor(V.ravel(order="F").copy()).to(ctx.device)
+    ctx.call("nkv_rotate", Q.ptr, k, Vd.data_ptr(), k, ctx.stream)
+    Qk = np.ascontiguousarray(Qref[:k])
+    orc.lib().orc_rotate(ctypes.byref(L.c), Qk, k, np.ascontiguousarray(V.ravel(order="F")))
+    got = Q.storage.cpu().numpy()
+    for i in range(k):
+        np.testing.assert_allclose(syn.to_reference_order(lay, got[i]), Qk[i], rtol=1e-12, atol=1e-13)
+        assert got[i][lay.time_offset] == 1.0 + i  # time not rotated
+    np.testing.assert_array_equal(syn.to_reference_order(lay, got[k]), Qref[k])  # column k untouched
+
+
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2"])
+@pytest.mark.parametrize("name", list(LAYOUTS))
+def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
+    lay = LAYOUTS[name]
+    ctx, w = make_ctx(lay, max_cols=32)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    m = 20
+    Q = ctx.basis(m + 1)
+    q0 = syn.hash_vector(lay, 5)
+    Q[0].from_packed(q0)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, m)
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode=mode)
+    H = Hd.download()
+
+    Qr = np.zeros((m + 1, L.len))
+    Qr[0] = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, Qr[0])
+    Hr = np.zeros((m + 1, m))
+    dref = syn.to_reference_order(lay, d)
+    orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.0),
+                              Qr, Hr, 1, m)
+    assert np.max(np.abs(H - Hr)) <= 1e-12 * np.max(np.abs(Hr)), np.max(np.abs(H - Hr))
+    Qg = Q.storage.cpu().numpy()
+    for i in range(m + 1):
+        np.testing.assert_allclose(syn.to_reference_order(lay, Qg[i]), Qr[i], rtol=0, atol=1e-10)
+    # orthonormality in the W inner product (orthonormality.dat check, eigensolvers.f90:335-345)
+    G = np.array([[ctx.dot(Q[a], Q[b], time=False) for b in range(m + 1)] for a in range(m + 1)])
+    assert np.max(np.abs(G - np.eye(m + 1))) < 1e-13
+
+
+def test_rot2_operator_vs_numpy(gpu):
+    lay = LAYOUTS["3d_scalar"]
+    ctx, _ = make_ctx(lay)
+    c, s, dr, _ = syn.rot2_operator(lay)
+    op = Rot2Operator(ctx, c, s, dr)
+    from helpers import oracle_rot2_matvec
+    x = syn.hash_vector(lay, 9)
+    xr = syn.to_reference_order(lay, x)
+    for tr in (False, True):
+        y = ctx.vector()
+        (op.rmatvec if tr else op.matvec)(dev_vec(ctx, x), y)
+        yr = np.zeros_like(xr)
+        oracle_rot2_matvec(lay, c, s, dr, tr)(xr, yr)
+        np.testing.assert_allclose(syn.to_reference_order(lay, y.to_packed()), yr, rtol=1e-15, atol=1e-16)
+
+
+def test_nan_is_reported(gpu):
+    lay = LAYOUTS["2d"]
+    ctx, _ = make_ctx(lay)
+    a = syn.hash_vector(lay, 1)
+    a[17] = np.nan
+    x = dev_vec(ctx, a)
+    with pytest.raises(NkvNaNError):
+        x.dot(x)
+    ctx.check_nan()  # flag was cleared
+
+
+def test_shape_errors(gpu):
+    lay = LAYOUTS["2d"]
+    ctx, _ = make_ctx(lay)
+    from nekstab_next_amd._lib import NkvError
+    v = ctx.vector()
+    with pytest.raises(NkvError):
+        ctx.call("nkv_block_dot", ctx.w.data_ptr(), v.ptr, 0, v.ptr, ctx.h1.data_ptr(), ctx.ws.data_ptr(), 0,
+                 ctx.stream)
+    with pytest.raises(NkvError):
+        ctx.call("nkv_rotate", v.ptr, 300, ctx.h1.data_ptr(), 300, ctx.stream)
