@@ -1,0 +1,230 @@
+#!/usr/bin/env python
+"""Benchmark: Arnoldi-step GB/s (achieved HBM) + Ritz-value relative error, N=1e8, m=128.
+
+BASELINE.json config 3: "Synthetic shift-invert Laplacian, N=1e8 dofs, m=128, basis sharded over
+MI355X GPUs with RCCL all-reduce" — 3-D spectral-element layout lx1=8, lx2=6, fields
+{vx, vy, vz, t} weighted + pressure, E=44,176 elements -> N = 100,014,464 doubles per vector
+(SURVEY.md §8(d)).  Total N is fixed for every GPU count (strong scaling): each rank owns an
+element-contiguous shard; dots are all-reduced (RCCL) once per Gram–Schmidt pass.
+
+One *step* = one full m-step Arnoldi factorisation from the normalised seed (prepare_seed, then
+m x [synthetic matvec + CGS2 Gram–Schmidt + normalise]) followed by the host Ritz extraction
+(H download, dgeev, residuals) — the work of one Krylov–Schur cycle before any restart.
+
+``value`` = whole-job algorithmic bytes / step time.  Bytes per Arnoldi step j:
+  B(j) = 8 [2j(N_w+N) + 2(N_w+n_v) + 4N + n_v + 2N]  plus the diagonal matvec 8*3N,
+summed over j = 1..m and over ranks (global N).  ``roofline`` is the dominant kernel family
+(block multi-dot or block update) timed live with HIP events on the launch stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+
+
+def step_bytes(N, N_w, n_v, m):
+    """Σ_j B(j) + matvec bytes over one m-step factorisation (global sizes)."""
+    tot = 0.0
+    for j in range(1, m + 1):
+        tot += 8.0 * (2 * j * (N_w + N) + 2 * (N_w + n_v) + 4 * N + n_v + 2 * N)
+        tot += 8.0 * 3 * N  # y = d .* x
+    return tot
+
+
+def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
+    """The reference algorithm (MGS + full re-orthogonalisation with per-field weighted dots, copy
+    -> dot -> cmult -> sub2, krylov_decomposition.f90:155-180) restated in C (oracle/), on the same
+    operator family at a bounded sample size, timed on this host.  Steps run until ``budget_s``."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+
+    import oracle as orc
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import box3d_layout
+
+    lay = box3d_layout(E_sample)
+    L = orc.OLayout(lay.n_v, lay.n_p, lay.n_wf, False, lay.ldim)
+    w = syn.mass_weights(lay)
+    d, _ = syn.laplacian_shift_invert(lay)
+    dref = syn.to_reference_order(lay, d)
+    orc.set_threads(threads)
+    Q = np.zeros((m + 1, L.len))
+    Q[0] = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 11)))
+    H = np.zeros((m + 1, m))
+    f = L.zeros()
+    wrk = L.zeros()
+    c = ctypes.byref(L.c)
+    done_bytes, t0, steps = 0.0, time.perf_counter(), 0
+    for j in range(1, m + 1):
+        orc.lib().orc_op_diag(c, dref, Q[j - 1], f, 0.0)
+        col = np.zeros(j + 1)
+        orc.lib().orc_update_hessenberg(c, w, col, f, Q[:j], j, wrk)  # Q rows are contiguous views
+        Q[j] = f
+        done_bytes += 8.0 * (2 * j * (lay.N_w + lay.N) + 2 * (lay.N_w + lay.n_v) + 4 * lay.N + lay.n_v + 2 * lay.N)
+        done_bytes += 8.0 * 3 * lay.N
+        steps = j
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    orc.set_threads(1)
+    return dict(value=done_bytes / dt / 1e9, unit="GB/s", cores=threads, kind="port",
+                sample=(f"reference MGS2 Arnoldi (C restatement, oracle/nekstab_oracle.c) on the same 3-D "
+                        f"lx1=8 layout at E={E_sample} (N={lay.N}), steps j=1..{steps} of m={m}, "
+                        f"{dt:.1f} s, {threads} OpenMP threads; bytes by the same CGS2 byte model"),
+                seconds=dt)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--E", type=int, default=44176, help="global elements (44,176 -> N=1.0e8)")
+    ap.add_argument("--m", type=int, default=128)
+    ap.add_argument("--mode", default="cgs2")
+    ap.add_argument("--cpu-E", type=int, default=512)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from nekstab_next_amd import lapack
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
+    from nekstab_next_amd.comm import init_from_env
+    from nekstab_next_amd.krylov_schur import prepare_seed
+    from nekstab_next_amd.layout import box3d_layout
+    from nekstab_next_amd.operators import DiagOperator
+    from nekstab_next_amd.profiling import PhaseTimer
+    from nekstab_next_amd.vector import NekContext
+
+    comm = init_from_env("nccl")
+    rank, world = comm.rank, comm.world
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    glay = box3d_layout(args.E)
+    lay = glay.shard(rank, world)
+    m = args.m
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, comm=comm, max_cols=m + 1, device=dev)
+    d, exact = syn.laplacian_shift_invert(lay)
+    op = DiagOperator(ctx, d)
+    del d
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    Q = ctx.basis(m + 1)
+    Hd = HessenbergDev(ctx, m)
+    f = ctx.vector()
+
+    def one_step():
+        prepare_seed(seed, Q[0])
+        arnoldi_factorization(ctx, op, Q, Hd, 1, m, f=f, mode=args.mode)
+        H = Hd.download()
+        vals, vecs = lapack.eig(H[:m, :m])
+        res = np.abs(H[m, m - 1] * vecs[m - 1, :])
+        return vals, res
+
+    for _ in range(args.warmup):
+        one_step()
+    timer = PhaseTimer(dev)
+    ctx.timer = timer
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        vals, res = one_step()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = comm.max_scalar(elapsed, device=dev)
+    ctx.timer = None
+    phases = timer.summary()
+    ctx.check_nan()
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bytes = step_bytes(glay.N, glay.N_w, glay.pts_v * glay.nelgv, m) * args.steps
+    value = total_bytes / elapsed / 1e9
+
+    # Ritz accuracy vs the exact spectrum of the synthetic operator
+    # (exact spectrum: the 4096 largest |mu|; a converged Ritz value is matched to the nearest one)
+    conv = res < 1e-6
+    errs = [float(np.min(np.abs(exact - v)) / abs(v)) for v in vals[conv]] if conv.any() else []
+    ritz_err = max(errs) if errs else None
+    top_err = float(np.max(np.abs(vals[:8] - exact[:8]) / np.abs(exact[:8])))
+
+    # dominant kernel family (rank-local launches; bytes are this rank's shard)
+    dom = max(("block_dot", "block_update"), key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
+    ph = phases[dom]
+    achieved = ph["gbps"]
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("kernel_family") == dom and tj.get("E") == args.E and tj.get("m") == m and world == 1:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(args.cpu_E, m, threads, args.cpu_budget)
+        out = {
+            "metric": "Arnoldi-step GB/s (achieved HBM) + Ritz-value rel-err, N=1e8 m=128",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (diagonalised shift-invert Laplacian, hashed seed, GLL x J_e weights)",
+            "config": {
+                "workload": "config3: m-step Arnoldi (CGS2) + Ritz extraction, shift-invert Laplacian",
+                "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
+                "m": m, "mode": args.mode, "parallelism": f"element-shard x{world} + RCCL allreduce",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "avg_launch_ms": round(ph["avg_ms"], 4),
+                "avg_bytes_per_launch": ph["avg_bytes"],
+                "launches": ph["launches"],
+            },
+            "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                       for k, v in phases.items()},
+            "ritz_rel_err": ritz_err,
+            "ritz_top8_rel_err": top_err,
+            "ritz_converged": int(conv.sum()),
+            "cpu_baseline": ({k: v for k, v in cpu.items() if k != "seconds"} if cpu else None),
+        }
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -60,13 +60,27 @@ def update_hessenberg_matrix(ctx: NekContext, Q: Basis, k: int, f: NekVector, Hd
     tf = NKV_TIME if ctx.time_in_dot else 0
     h1, h2, nrm = ctx.h1[:j], ctx.h2[:j], ctx.scal[3:4]
     if mode == "cgs2":
-        ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h1.data_ptr(), ws, tf, st)
-        ctx.comm.allreduce_(h1)
-        ctx.call("nkv_block_update", w, Q.ptr, j, h1.data_ptr(), f.ptr, None, ws, NKV_TIME, st)
-        ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h2.data_ptr(), ws, tf, st)
-        ctx.comm.allreduce_(h2)
-        ctx.call("nkv_block_update", w, Q.ptr, j, h2.data_ptr(), f.ptr, nrm.data_ptr(), ws,
-                 NKV_TIME | NKV_NORM2 | tf, st)
+        lay, tm = ctx.layout, ctx.timer
+        # algorithmic bytes: dot reads j weighted columns + f_w + w;
+        # update reads j full columns + f, writes f (+ w for the fused norm)
+        b_dot = 8.0 * (j * lay.N_w + lay.N_w + lay.n_v)
+        b_upd = 8.0 * (j * lay.N + 2 * lay.N)
+        for h, last in ((h1, False), (h2, True)):
+            if tm:
+                tm.begin("block_dot")
+            ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h.data_ptr(), ws, tf, st)
+            if tm:
+                tm.end("block_dot", b_dot)
+            ctx.comm.allreduce_(h)
+            if tm:
+                tm.begin("block_update")
+            if last:
+                ctx.call("nkv_block_update", w, Q.ptr, j, h.data_ptr(), f.ptr, nrm.data_ptr(), ws,
+                         NKV_TIME | NKV_NORM2 | tf, st)
+            else:
+                ctx.call("nkv_block_update", w, Q.ptr, j, h.data_ptr(), f.ptr, None, ws, NKV_TIME, st)
+            if tm:
+                tm.end("block_update", b_upd + (8.0 * lay.n_v if last else 0.0))
         ctx.comm.allreduce_(nrm)
     elif mode == "mgs2":
         for h in (h1, h2):
@@ -79,8 +93,12 @@ def update_hessenberg_matrix(ctx: NekContext, Q: Basis, k: int, f: NekVector, Hd
         ctx.comm.allreduce_(nrm)
     else:
         raise ValueError(f"unknown orthogonalisation mode {mode!r}")
+    if ctx.timer:
+        ctx.timer.begin("finish")
     ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), Q.col_ptr(j), j, h1.data_ptr(), h2.data_ptr(),
              Hd.col_ptr(j - 1), 0, st)
+    if ctx.timer:
+        ctx.timer.end("finish", 16.0 * ctx.layout.N)
 
 
 def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,

@@ -180,7 +180,7 @@ def _affine_perm_params(n: int, seed: int) -> tuple[int, int]:
 
 
 def laplacian_shift_invert(lay: NekLayout, seed: int = 3, k0: int = 3, frac: float = 0.3,
-                           pr_value: float = 0.1, n_exact: int = 12):
+                           pr_value: float = 0.1, n_exact: int = 4096):
     """(padded diag, exact top-|mu| eigenvalues).  mu_g = 1/(lambda_{pi(g)} - sigma) with the
     1-D Dirichlet Laplacian spectrum lambda_k = -4 sin^2(k pi / (2(n+1))), k = 1..n (n = global
     weighted dofs), pi(g) = (a g + b) mod n + 1, sigma = lambda_k0 + frac (lambda_{k0+1} - lambda_k0)."""
@@ -198,7 +198,8 @@ def laplacian_shift_invert(lay: NekLayout, seed: int = 3, k0: int = 3, frac: flo
         d[f * lay.sv: f * lay.sv + lay.n_v] = 1.0 / (lam(k.astype(np.float64)) - sigma)
     s = lay.n_wf * lay.sv
     d[s: s + lay.n_p] = pr_value
-    ks = np.arange(1, min(n, k0 + 4 * n_exact) + 1, dtype=np.float64)
+    # |mu_k| decays like 1/k^2 away from k0, so the n_exact largest are among k <= k0 + 2 n_exact
+    ks = np.arange(1, min(n, k0 + 2 * n_exact + 8) + 1, dtype=np.float64)
     mu = 1.0 / (lam(ks) - sigma)
-    exact = mu[np.argsort(-np.abs(mu))][:n_exact]
+    exact = mu[np.argsort(-np.abs(mu), kind="stable")][:n_exact]
     return d, exact

@@ -53,6 +53,7 @@ class NekContext:
         self._Lp = ctypes.byref(self.L)
         self.time_in_dot = time_in_dot
         self.max_cols = max_cols
+        self.timer = None  # optional profiling.PhaseTimer (per-phase HIP events)
         self.lib = _lib.load()
         f64 = dict(dtype=torch.float64, device=self.device)
         self.w = torch.zeros(layout.sv, **f64)
