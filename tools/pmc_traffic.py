@@ -1,0 +1,67 @@
+#!/usr/bin/env python
+"""Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, MI355X_MICROARCH.md
+§HBM) of ``bench.py`` into per-launch HBM traffic per kernel family.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7): counters are in KiB;
+FETCH_SIZE reports exactly half of a wide (16 B/lane) coalesced streaming read, so it is doubled
+(all our streaming loads are 16 B/lane double2 loads; the copy kernel k_blas1<COPY> calibrates it:
+N*8 bytes read -> FETCH_SIZE*2*1024); WRITE_SIZE is exact for 16 B/lane stores.
+
+usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+FAMILIES = {
+    "block_dot": ("k_block_dot",),
+    "block_update": ("k_block_update",),
+    "update_dot": ("k_update_dot",),
+    "finish": ("k_finish",),
+    "op_diag": ("k_op_diag",),
+    "copy": ("k_blas1<1>",),
+}
+
+
+def load(d):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        out[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def fam_of(name):
+    for fam, keys in FAMILIES.items():
+        if any(k in name for k in keys):
+            return fam
+    return None
+
+
+def main():
+    fdir, wdir, bench_json, out_json = sys.argv[1:5]
+    F, W = load(fdir), load(wdir)
+    bench = json.load(open(bench_json))
+    agg = {}
+    for fam in FAMILIES:
+        fv = [v for k, vs in F.items() if fam_of(k) == fam for v in vs]
+        wv = [v for k, vs in W.items() if fam_of(k) == fam for v in vs]
+        if not fv:
+            continue
+        rd = 2.0 * 1024.0 * sum(fv) / len(fv)
+        wr = 1024.0 * sum(wv) / len(wv) if wv else 0.0
+        agg[fam] = dict(launches=len(fv), read_bytes_per_launch=rd, write_bytes_per_launch=wr,
+                        hbm_bytes_per_launch=rd + wr)
+    dom = bench["roofline"]["kernel"]
+    rec = dict(kernel_family=dom, E=bench["config"]["E"], m=bench["config"]["m"],
+               hbm_bytes_per_launch=agg.get(dom, {}).get("hbm_bytes_per_launch"),
+               algorithmic_bytes_per_launch=bench["roofline"]["avg_bytes_per_launch"],
+               families=agg, correction="FETCH_SIZE x2 (16 B/lane streaming reads on gfx950), KiB -> bytes",
+               source=[fdir, wdir])
+    json.dump(rec, open(out_json, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
