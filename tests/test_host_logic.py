@@ -1,0 +1,97 @@
+"""Host-side restart logic: the product's Python restatement (nekstab_next_amd.lapack) against the
+oracle's independent C transliteration of the same Fortran (CPU only)."""
+import numpy as np
+import pytest
+
+import oracle as orc
+from nekstab_next_amd import lapack
+
+
+def _spectrum(rng, n, pairs=True, ties=False):
+    vals = []
+    while len(vals) < n:
+        r = rng.uniform(0.0, 1.0)
+        if pairs and len(vals) <= n - 2 and rng.random() < 0.4:
+            t = rng.uniform(0.1, 3.0)
+            vals += [r * np.exp(1j * t), r * np.exp(-1j * t)]
+        else:
+            vals.append(complex(rng.choice([-1, 1]) * r, 0.0))
+    v = np.asarray(vals[:n])
+    if ties:
+        v[: n // 3] = np.round(v[: n // 3].real, 1)
+    return v
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 33, 64, 100, 128, 200])
+def test_quicksort2_python_equals_c(n):
+    rng = np.random.default_rng(n)
+    for t in range(30):
+        arr = rng.integers(0, 5, n).astype(float) if t % 3 == 0 else rng.random(n)
+        idx_c, _ = orc.quicksort2(arr)
+        np.testing.assert_array_equal(lapack.quicksort2(arr), idx_c)
+
+
+def test_quicksort2_small_n_sorts_and_known_quirk():
+    rng = np.random.default_rng(1)
+    for n in range(1, 8):  # below the insertion-sort threshold the result is a true argsort
+        a = rng.random(n)
+        assert np.all(np.diff(a[lapack.quicksort2(a)]) >= 0)
+    # n >= 8: the partition overwrites the pivot slot (utils.f90:106-109) -> index 1 lost, 0 doubled
+    x = np.array([3.0, 1.0, 2.0, 0.5, 7.0, 6.0, 5.0, 4.0])
+    assert lapack.quicksort2(x).tolist() == [3, 2, 0, 0, 7, 6, 5, 4]
+
+
+@pytest.mark.parametrize("k", [10, 16, 24, 64, 128])
+@pytest.mark.parametrize("nev", [1, 2, 5])
+def test_select_eigenvalues_python_equals_c(k, nev):
+    rng = np.random.default_rng(k * 10 + nev)
+    for t in range(20):
+        vals = _spectrum(rng, k, pairs=(t % 2 == 0), ties=(t % 5 == 0))
+        s_c, c_c = orc.select_eigenvalues(vals, 0.1, nev)
+        s_p, c_p = lapack.select_eigenvalues(vals, 0.1, nev)
+        np.testing.assert_array_equal(s_p, s_c)
+        assert c_p == c_c
+
+
+def test_select_eigenvalues_real_boundary_quirk():
+    """Two real eigenvalues at the nev+4 boundary: 0 == -0 selects one more (eigensolvers.f90:747)."""
+    vals = np.array([0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7], dtype=complex)
+    sel, cnt = lapack.select_eigenvalues(vals, 0.1, 1, faithful=False)
+    assert cnt == 6  # nev+4 = 5 largest + 1 via the imaginary-part equality
+    sel_c, cnt_c = orc.select_eigenvalues(vals, 0.1, 1)
+    assert cnt_c == cnt
+
+
+@pytest.mark.parametrize("n", [5, 16, 40])
+def test_eig_and_sort_python_equals_oracle(n):
+    rng = np.random.default_rng(n)
+    A = np.triu(rng.standard_normal((n, n)), -1)  # upper Hessenberg
+    v1, V1 = lapack.eig(A)
+    v2, V2 = orc.eig(A)
+    np.testing.assert_array_equal(v1, v2)
+    np.testing.assert_array_equal(V1, V2)
+    # eigen-relation A V = V diag(v)
+    assert np.max(np.abs(A @ V1 - V1 * v1)) < 1e-10 * max(1, np.abs(v1).max())
+    assert np.all(np.diff(np.abs(v1)) <= 1e-15)
+
+
+def test_schur_ordschur_lstsq():
+    rng = np.random.default_rng(3)
+    n = 20
+    A = np.triu(rng.standard_normal((n, n)), -1) * 0.3
+    A[0, 0] = 0.98
+    T, Z, vals = lapack.schur(A)
+    T2, Z2, vals2 = orc.schur_sorted(A)
+    np.testing.assert_array_equal(T, T2)
+    np.testing.assert_array_equal(Z, Z2)
+    assert np.max(np.abs(Z @ T @ Z.T - A)) < 1e-12
+    sel, cnt = lapack.select_eigenvalues(vals, 0.1, 2)
+    Ts, Zs, m = lapack.ordschur(T, Z, sel)
+    Ts2, Zs2 = orc.ordschur(T2, Z2, sel)
+    np.testing.assert_array_equal(Ts, Ts2)
+    assert m == cnt
+    assert np.max(np.abs(Zs @ Ts @ Zs.T - A)) < 1e-12
+    B = rng.standard_normal((n + 1, n))
+    b = rng.standard_normal(n + 1)
+    np.testing.assert_allclose(lapack.lstsq(B, b), np.linalg.lstsq(B, b, rcond=None)[0], rtol=1e-10)
+    np.testing.assert_array_equal(lapack.lstsq(B, b), orc.lstsq(B, b))

@@ -1,0 +1,116 @@
+"""Layout/shard arithmetic, shard-independent generators, and the C ABI surface (CPU only: the
+library is loaded and its exports checked; no compute entry point is called without a GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from nekstab_next_amd import synthetic as syn
+from nekstab_next_amd.layout import NKV_TILE, NekLayout, box3d_layout, cylinder_layout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_baseline_config_sizes():
+    assert cylinder_layout(1996).N == 175648 and cylinder_layout(1996).N_w == 143712
+    assert cylinder_layout(22728).N == 2000064
+    c3 = box3d_layout(44176)
+    assert (c3.n_v, c3.N_w, c3.n_p, c3.N) == (22618112, 90472448, 9542016, 100014464)
+    assert box3d_layout(22088).N == 50007232
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_shards_partition_elements(world):
+    g = box3d_layout(44176)
+    shards = [g.shard(r, world) for r in range(world)]
+    assert sum(s.nelv for s in shards) == g.nelgv
+    assert sum(s.N for s in shards) == g.N
+    off = 0
+    for s in shards:
+        assert s.v_offset == off * g.pts_v and s.p_offset == off * g.pts_p
+        off += s.nelv
+        assert s.sv % NKV_TILE == 0 and s.sp % NKV_TILE == 0 and s.ld % NKV_TILE == 0
+        assert s.sv >= s.n_v and s.ld >= s.rows + 1
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_generators_are_shard_independent(world):
+    g = NekLayout(ldim=3, lx1=4, lx2=2, nelgv=13, n_scalars=1)
+    full = syn.to_reference_order(g, syn.hash_vector(g, 77))
+    dfull, _ = syn.laplacian_shift_invert(g)
+    dfull = syn.to_reference_order(g, dfull)
+    wfull = syn.mass_weights(g)
+    parts = {f: [] for f in range(g.n_wf + 1)}
+    dparts = {f: [] for f in range(g.n_wf + 1)}
+    wparts = []
+    for r in range(world):
+        s = g.shard(r, world)
+        v = syn.to_reference_order(s, syn.hash_vector(s, 77))
+        d, _ = syn.laplacian_shift_invert(s)
+        d = syn.to_reference_order(s, d)
+        for f in range(g.n_wf):
+            parts[f].append(v[f * s.n_v:(f + 1) * s.n_v])
+            dparts[f].append(d[f * s.n_v:(f + 1) * s.n_v])
+        parts[g.n_wf].append(v[g.n_wf * s.n_v: g.n_wf * s.n_v + s.n_p])
+        dparts[g.n_wf].append(d[g.n_wf * s.n_v: g.n_wf * s.n_v + s.n_p])
+        wparts.append(syn.mass_weights(s))
+    cat = np.concatenate([np.concatenate(parts[f]) for f in range(g.n_wf + 1)] + [np.zeros(1)])
+    np.testing.assert_array_equal(cat, full)
+    dcat = np.concatenate([np.concatenate(dparts[f]) for f in range(g.n_wf + 1)] + [np.zeros(1)])
+    np.testing.assert_array_equal(dcat, dfull)
+    np.testing.assert_array_equal(np.concatenate(wparts), wfull)
+
+
+def test_host_generator_matches_oracle_c_and_numpy():
+    g = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=50)
+    L = orc.OLayout(g.n_v, g.n_p, g.n_wf)
+    a = syn.to_reference_order(g, syn.hash_vector(g, 5))
+    np.testing.assert_array_equal(a, orc.fill_hash(L, 5))
+    np.testing.assert_array_equal(a, orc.fill_hash_np(g.n_wf, g.n_v, g.n_p, 5))
+
+
+def test_gll_weights():
+    for n in range(2, 12):
+        w = syn.gll_weights(n)
+        assert abs(w.sum() - 2.0) < 1e-13 and np.all(w > 0)
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "nekkrylov.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(nkv_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from nekstab_next_amd import _lib
+
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_lib.EXPORTED) == syms  # the ctypes table types every declared entry point
+    assert lib.nkv_abi_version() == 1
+
+
+def test_workspace_size_is_host_only():
+    from nekstab_next_amd import _lib
+
+    lib = _lib.load()
+    L = box3d_layout(100).c_struct()
+    n = lib.nkv_workspace_bytes(ctypes.byref(L), 128)
+    assert n >= 256 + 8 * 128
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from nekstab_next_amd.vector import NekContext
+
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        NekContext(NekLayout(ldim=2, lx1=4, lx2=2, nelgv=4))
