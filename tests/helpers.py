@@ -45,3 +45,20 @@ def match_ritz(a, b):
         j = int(np.argmin([abs(x - y) for y in b]))
         out.append(b.pop(j))
     return np.asarray(out)
+
+
+def oracle_rank2_matvec(lay, d, u, v, u2, v2, sigma, w, transpose=False):
+    """Reference-order twin of operators.RankTwoPerturbed: D x + sigma (u <v,x>_W + u2 <v2,x>_W)."""
+    L = olayout(lay)
+    dr = syn.to_reference_order(lay, d)
+    U, V, U2, V2 = (syn.to_reference_order(lay, a) for a in (u, v, u2, v2))
+    if transpose:
+        U, V, U2, V2 = V, U, V2, U2
+
+    def mv(x, y):
+        a = orc.k_dot(L, w, V, x)
+        b = orc.k_dot(L, w, U2, x)
+        y[:] = dr * x
+        y[-1] = 0.0
+        y[:-1] += sigma * (U[:-1] * a + V2[:-1] * b)
+    return mv
