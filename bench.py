@@ -11,10 +11,14 @@ One *step* = one full m-step Arnoldi factorisation from the normalised seed (pre
 m x [synthetic matvec + CGS2 Gram–Schmidt + normalise]) followed by the host Ritz extraction
 (H download, dgeev, residuals) — the work of one Krylov–Schur cycle before any restart.
 
-``value`` = whole-job algorithmic bytes / step time.  Bytes per Arnoldi step j:
-  B(j) = 8 [2j(N_w+N) + 2(N_w+n_v) + 4N + n_v + 2N]  plus the diagonal matvec 8*3N,
-summed over j = 1..m and over ranks (global N).  ``roofline`` is the dominant kernel family
-(block multi-dot or block update) timed live with HIP events on the launch stream.
+``value`` = achieved HBM GB/s of the whole step: the bytes the executed algorithm moves (global N,
+all ranks; see ``executed_bytes``) / step time.  The fused CGS2 reads the basis 3x per Arnoldi
+step, so it moves fewer bytes than SURVEY.md §8(d)'s 4-pass model
+  B(j) = 8 [2j(N_w+N) + 2(N_w+n_v) + 4N + n_v + 2N]  (+ 8*3N matvec);
+that model divided by the same time is reported separately as ``effective_gbs_survey_model`` (the
+work definition the CPU baseline is also measured in).  ``roofline`` is the dominant kernel family
+(block multi-dot, fused update+dot, or update+norm) timed live with HIP events on the launch
+stream.
 """
 from __future__ import annotations
 
@@ -32,12 +36,31 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 
 
-def step_bytes(N, N_w, n_v, m):
-    """Σ_j B(j) + matvec bytes over one m-step factorisation (global sizes)."""
+def survey_model_bytes(N, N_w, n_v, m):
+    """SURVEY.md §8(d) byte model of a 4-pass CGS2 step, Σ_j B(j), plus the matvec (8*3N per step).
+    Used for the CPU baseline and as the *effective* rate of the GPU (same work definition)."""
     tot = 0.0
     for j in range(1, m + 1):
         tot += 8.0 * (2 * j * (N_w + N) + 2 * (N_w + n_v) + 4 * N + n_v + 2 * N)
-        tot += 8.0 * 3 * N  # y = d .* x
+        tot += 8.0 * 3 * N
+    return tot
+
+
+def executed_bytes(N, N_w, n_v, m, mode):
+    """HBM bytes the executed algorithm moves per factorisation (global sizes), per kernel:
+    block_dot 8(jN_w + N_w + n_v); fused update_dot 8(jN + 2N + n_v); update+norm 8(jN + 2N + n_v);
+    finish 8(2N); diag matvec 8(3N).  (PMC FETCH/WRITE_SIZE agree within 1%, profiles/.)"""
+    tot = 0.0
+    for j in range(1, m + 1):
+        dot = 8.0 * (j * N_w + N_w + n_v)
+        upd = 8.0 * (j * N + 2 * N)
+        if mode == "cgs2":
+            tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
+        elif mode == "cgs2-unfused":
+            tot += 2 * dot + upd + (upd + 8.0 * n_v)
+        else:
+            raise ValueError(mode)
+        tot += 8.0 * 2 * N + 8.0 * 3 * N
     return tot
 
 
@@ -80,7 +103,8 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
     return dict(value=done_bytes / dt / 1e9, unit="GB/s", cores=threads, kind="port",
                 sample=(f"reference MGS2 Arnoldi (C restatement, oracle/nekstab_oracle.c) on the same 3-D "
                         f"lx1=8 layout at E={E_sample} (N={lay.N}), steps j=1..{steps} of m={m}, "
-                        f"{dt:.1f} s, {threads} OpenMP threads; bytes by the same CGS2 byte model"),
+                        f"{dt:.1f} s, {threads} OpenMP threads; GB/s in SURVEY.md §8(d)'s CGS2 byte model "
+                        f"(compare with effective_gbs_survey_model)"),
                 seconds=dt)
 
 
@@ -157,8 +181,9 @@ def main():
     ctx.check_nan()
 
     ms_per_step = elapsed / args.steps * 1e3
-    total_bytes = step_bytes(glay.N, glay.N_w, glay.pts_v * glay.nelgv, m) * args.steps
-    value = total_bytes / elapsed / 1e9
+    nv_g = glay.pts_v * glay.nelgv
+    value = executed_bytes(glay.N, glay.N_w, nv_g, m, args.mode) * args.steps / elapsed / 1e9
+    effective = survey_model_bytes(glay.N, glay.N_w, nv_g, m) * args.steps / elapsed / 1e9
 
     # Ritz accuracy vs the exact spectrum of the synthetic operator
     # (exact spectrum: the 4096 largest |mu|; a converged Ritz value is matched to the nearest one)
@@ -168,7 +193,7 @@ def main():
     top_err = float(np.max(np.abs(vals[:8] - exact[:8]) / np.abs(exact[:8])))
 
     # dominant kernel family (rank-local launches; bytes are this rank's shard)
-    dom = max(("block_dot", "block_update"), key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
+    dom = max(("block_dot", "update_dot", "block_update"), key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
     ph = phases[dom]
     achieved = ph["gbps"]
     traffic = None
@@ -194,6 +219,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            "effective_gbs_survey_model": round(effective, 2),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

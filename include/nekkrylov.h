@@ -65,6 +65,7 @@ extern "C" {
 #define NKV_ACCUMULATE 0x2u /* block_update: f <- f - Q h   (default)                             */
 #define NKV_OVERWRITE 0x4u  /* block_update: f <- + Q h     (k_matmul, krylov_subspace.f90:163)    */
 #define NKV_NORM2 0x8u      /* block_update: also write the local ||f||_W^2 partial               */
+#define NKV_TIME_DOT 0x10u  /* block_update_dot: include the time product in the dot partial      */
 
 typedef struct nkv_layout {
     int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */
@@ -124,6 +125,10 @@ int nkv_block_dot(const nkv_layout* L, const double* w, const double* Q, int j, 
                   double* h_dev, void* ws, unsigned flags, void* stream);
 int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
                      double* f, double* nrm2_dev, void* ws, unsigned flags, void* stream);
+/* Fused CGS2 middle pass (one read of Q): f <- f - Q[:,0:j] h, then hout_dev[0:j] = Q^T W f_new
+ * (LOCAL partials).  NKV_TIME updates f.time, NKV_TIME_DOT adds the time product to hout (rank0). */
+int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
+                         double* f, double* hout_dev, void* ws, unsigned flags, void* stream);
 int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,
                        int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
                        unsigned flags, void* stream);

@@ -23,6 +23,7 @@ NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2
 NKV_OVERWRITE = 0x4
 NKV_NORM2 = 0x8
+NKV_TIME_DOT = 0x10
 
 
 class NkvError(RuntimeError):
@@ -69,6 +70,7 @@ _SIGNATURES = {
     "nkv_dot": (c_int, [_L, _P, _P, _P, _P, _P, c_uint, _P]),
     "nkv_block_dot": (c_int, [_L, _P, _P, c_int, _P, _P, _P, c_uint, _P]),
     "nkv_block_update": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
+    "nkv_block_update_dot": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_arnoldi_finish": (c_int, [_L, _P, _P, _P, c_int, _P, _P, _P, c_uint, _P]),
     "nkv_rotate": (c_int, [_L, _P, c_int, _P, c_int, _P]),
     "nkv_op_diag": (c_int, [_L, _P, _P, _P, c_double, _P]),

@@ -10,10 +10,12 @@ Q(k+1) <- f (:81).
 Two orthogonalisation modes share the rest of the path:
 
 * ``"cgs2"`` (default, the MI355X hot path): block classical Gram–Schmidt applied twice —
-  ``h1 = Q^T W f`` (one fused multi-dot kernel + ONE length-j all-reduce), ``f -= Q h1``, the same
-  again for ``h2``, the second update fusing the ||f||_W^2 partial, then one kernel writing
-  q_{k+1} = f/||f|| and the H column (h1 + h2, ||f||) on the device.  ~4j(N) streamed doubles per
-  step instead of the reference's ~20jN, and 3 collectives instead of (2k+2)*n_fields.
+  ``h1 = Q^T W f`` (one multi-dot kernel + ONE length-j all-reduce); then ``f -= Q h1`` fused with
+  ``h2 = Q^T W f`` in a single read of Q (+ all-reduce); ``f -= Q h2`` with the ||f||_W^2 partial
+  fused (+ all-reduce); one kernel writing q_{k+1} = f/||f|| and the H column (h1 + h2, ||f||) on
+  the device.  ~3jN streamed doubles per step instead of the reference's ~20jN, and 3
+  collectives instead of (2k+2)*n_fields.  ``"cgs2-unfused"`` runs the middle pass as two kernels
+  (4 reads of Q), kept for A/B measurement.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
 
@@ -24,7 +26,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import NKV_NORM2, NKV_TIME
+from ._lib import NKV_NORM2, NKV_TIME, NKV_TIME_DOT
 from .operators import LinearOperator
 from .vector import Basis, NekContext, NekVector
 
@@ -59,28 +61,42 @@ def update_hessenberg_matrix(ctx: NekContext, Q: Basis, k: int, f: NekVector, Hd
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     tf = NKV_TIME if ctx.time_in_dot else 0
     h1, h2, nrm = ctx.h1[:j], ctx.h2[:j], ctx.scal[3:4]
-    if mode == "cgs2":
+    if mode in ("cgs2", "cgs2-unfused"):
         lay, tm = ctx.layout, ctx.timer
-        # algorithmic bytes: dot reads j weighted columns + f_w + w;
-        # update reads j full columns + f, writes f (+ w for the fused norm)
+        # algorithmic bytes: a dot reads j weighted columns + f_w + w; an update
+        # reads j full columns + f and writes f (+ w for the fused norm)
         b_dot = 8.0 * (j * lay.N_w + lay.N_w + lay.n_v)
         b_upd = 8.0 * (j * lay.N + 2 * lay.N)
-        for h, last in ((h1, False), (h2, True)):
+        if tm:
+            tm.begin("block_dot")
+        ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h1.data_ptr(), ws, tf, st)
+        if tm:
+            tm.end("block_dot", b_dot)
+        ctx.comm.allreduce_(h1)
+        if mode == "cgs2":  # f -= Q h1 and h2 = Q^T W f in ONE pass over Q
             if tm:
-                tm.begin("block_dot")
-            ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h.data_ptr(), ws, tf, st)
+                tm.begin("update_dot")
+            ctx.call("nkv_block_update_dot", w, Q.ptr, j, h1.data_ptr(), f.ptr, h2.data_ptr(), ws,
+                     NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
             if tm:
-                tm.end("block_dot", b_dot)
-            ctx.comm.allreduce_(h)
+                tm.end("update_dot", b_upd + 8.0 * lay.n_v)
+        else:
             if tm:
                 tm.begin("block_update")
-            if last:
-                ctx.call("nkv_block_update", w, Q.ptr, j, h.data_ptr(), f.ptr, nrm.data_ptr(), ws,
-                         NKV_TIME | NKV_NORM2 | tf, st)
-            else:
-                ctx.call("nkv_block_update", w, Q.ptr, j, h.data_ptr(), f.ptr, None, ws, NKV_TIME, st)
+            ctx.call("nkv_block_update", w, Q.ptr, j, h1.data_ptr(), f.ptr, None, ws, NKV_TIME, st)
             if tm:
-                tm.end("block_update", b_upd + (8.0 * lay.n_v if last else 0.0))
+                tm.end("block_update", b_upd)
+                tm.begin("block_dot")
+            ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h2.data_ptr(), ws, tf, st)
+            if tm:
+                tm.end("block_dot", b_dot)
+        ctx.comm.allreduce_(h2)
+        if tm:
+            tm.begin("block_update")
+        ctx.call("nkv_block_update", w, Q.ptr, j, h2.data_ptr(), f.ptr, nrm.data_ptr(), ws,
+                 NKV_TIME | NKV_NORM2 | tf, st)
+        if tm:
+            tm.end("block_update", b_upd + 8.0 * lay.n_v)
         ctx.comm.allreduce_(nrm)
     elif mode == "mgs2":
         for h in (h1, h2):

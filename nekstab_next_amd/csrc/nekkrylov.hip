@@ -280,6 +280,87 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
 }
 
 // ------------------------------------------------------------------------------------------
+// Fused CGS2 middle pass:  f <- f - Q h  AND  partials[c][b] = q_c . (w f_new)  in ONE read of Q.
+// A 512-thread workgroup owns 128-row tiles (lane = 2 rows, double2); its 8 waves split the j
+// columns (wave v holds columns v, v+8, ...: CPW double2 per lane in registers).  The per-wave
+// partial sums of Q h meet in LDS, every wave forms f_new for its rows, and the same registers
+// then feed the second projection, accumulated per lane across all tiles of the workgroup and
+// reduced across lanes once at the end.
+// ------------------------------------------------------------------------------------------
+constexpr int kFuseRows = 128;
+
+template <int NW, int CPW>
+__global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict__ Q, int64_t ld, int j,
+                                                         const double* __restrict__ h,
+                                                         double* __restrict__ f,
+                                                         const double* __restrict__ w, int64_t sv,
+                                                         int64_t tiles_per_field, int64_t tiles_w,
+                                                         int64_t tiles_total, int64_t time_off,
+                                                         int do_time, double* __restrict__ partials,
+                                                         int B) {
+    __shared__ double2 part[NW][64];
+    // wave index made provably uniform: column bases become scalar registers, the per-lane part of
+    // every address is one 32-bit row offset
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (do_time && blockIdx.x == 0 && wv == 0) {  // scalar time component of f (k_sub2 keeps it)
+        double s = 0.0;
+        for (int c = lane; c < j; c += 64) s = fma(Q[time_off + (int64_t)c * ld], h[c], s);
+        s = wave_sum(s);
+        if (lane == 0) f[time_off] -= s;
+    }
+    const double* qcol[CPW];
+    double hc[CPW];
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+        const int c = wv + NW * i;
+        qcol[i] = Q + (int64_t)(c < j ? c : 0) * ld;
+        hc[i] = c < j ? h[c] : 0.0;
+    }
+    double acc[CPW];
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) acc[i] = 0.0;
+    for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const uint32_t r = (uint32_t)(t * kFuseRows) + 2u * lane;
+        double2 q[CPW];
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) q[i] = ld2(qcol[i] + r);
+        double2 s = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) {
+            s.x = fma(hc[i], q[i].x, s.x);
+            s.y = fma(hc[i], q[i].y, s.y);
+        }
+        const double2 fv = ld2(f + r);
+        part[wv][lane] = s;
+        __syncthreads();
+        double2 tot = part[0][lane];
+#pragma unroll
+        for (int k = 1; k < NW; ++k) {
+            const double2 p = part[k][lane];
+            tot.x += p.x;
+            tot.y += p.y;
+        }
+        const double2 f1 = make_double2(fv.x - tot.x, fv.y - tot.y);
+        if (wv == 0) st2(f + r, f1);
+        if (t < tiles_w) {
+            const uint32_t wr = r - (uint32_t)((t / tiles_per_field) * sv);
+            const double2 ww = ld2(w + wr);
+            const double a = ww.x * f1.x, b = ww.y * f1.y;
+#pragma unroll
+            for (int i = 0; i < CPW; ++i) acc[i] = fma(q[i].y, b, fma(q[i].x, a, acc[i]));
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+        const int c = wv + NW * i;
+        const double v = wave_sum(acc[i]);
+        if (lane == 0 && c < j) partials[(int64_t)c * B + blockIdx.x] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Arnoldi finish / normalise:  q = f / sqrt(nrm2)  (all rows + time), H column on the device.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_finish(const double* f,  // may alias q (in-place)
@@ -711,6 +792,50 @@ int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int 
                            tdot ? f + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nan_flag_of(ws));
         NKV_LAUNCHED();
     }
+    return NKV_OK;
+}
+
+int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
+                         double* f, double* hout_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!h_dev || !hout_dev) return fail(NKV_EINVAL, "h_dev/hout_dev is NULL");
+    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    const unsigned upd_flags = (flags & NKV_TIME) ? NKV_TIME : 0u;
+    const unsigned dot_flags = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+    if (j > 256 || rows_of(L) >= (int64_t)1 << 32) {  // tile does not fit registers: two passes
+        CHECK(nkv_block_update(L, w, Q, j, h_dev, f, nullptr, ws, upd_flags, stream));
+        return launch_block_dot(L, w, Q, L->ld, j, f, hout_dev, ws, dot_flags, S(stream));
+    }
+    const int64_t rows = rows_of(L);
+    const int64_t tiles_total = rows / kFuseRows;
+    const int64_t tpf = L->sv / kFuseRows;
+    const int64_t tiles_w = tpf * L->n_wf;
+    int64_t g = tiles_total < 1024 ? tiles_total : 1024;
+    if (g < 1) g = 1;
+    const int B = (int)g;
+    const int64_t T = rows;
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    double* part = partials_of(ws);
+    hipStream_t st = S(stream);
+#define NKV_FUSE(NW, CPW)                                                                                     \
+    hipLaunchKernelGGL((k_update_dot<NW, CPW>), dim3((unsigned)g), dim3(NW * 64), 0, st, Q, L->ld, j, h_dev, f, w, \
+                       L->sv, tpf, tiles_w, tiles_total, T, dt, part, B)
+    if (j <= 8) NKV_FUSE(8, 1);
+    else if (j <= 16) NKV_FUSE(8, 2);
+    else if (j <= 32) NKV_FUSE(8, 4);
+    else if (j <= 64) NKV_FUSE(8, 8);
+    else if (j <= 128) NKV_FUSE(8, 16);
+    else NKV_FUSE(16, 16);
+#undef NKV_FUSE
+    NKV_LAUNCHED();
+    const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, B, hout_dev, tdot ? Q + T : nullptr,
+                       L->ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
     return NKV_OK;
 }
 

@@ -201,7 +201,7 @@ def test_rotate_vs_oracle(gpu, k):
     np.testing.assert_array_equal(syn.to_reference_order(lay, got[k]), Qref[k])  # column k untouched
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     lay = LAYOUTS[name]
@@ -271,3 +271,33 @@ def test_shape_errors(gpu):
                  ctx.stream)
     with pytest.raises(NkvError):
         ctx.call("nkv_rotate", v.ptr, 300, ctx.h1.data_ptr(), 300, ctx.stream)
+
+
+@pytest.mark.parametrize("j", [1, 5, 8, 9, 31, 64, 65, 128, 129, 200, 256, 300])
+def test_block_update_dot_fused_vs_numpy(gpu, j):
+    """nkv_block_update_dot = update then weighted multi-dot, in one pass (all CPW variants +
+    the two-pass fallback above 256 columns)."""
+    lay = LAYOUTS["3d_scalar"]
+    ctx, w = make_ctx(lay, max_cols=300)
+    Q = ctx.basis(j)
+    for i in range(j):
+        Q[i].fill_hash(300 + i)
+        Q[i].time = 0.01 * i
+    f = ctx.vector()
+    f.fill_hash(7)
+    f.time = 0.5
+    Qh = Q.storage.cpu().numpy()
+    fh = f.to_packed()
+    wfull = np.zeros(lay.ld)
+    for f_ in range(lay.n_wf):
+        wfull[f_ * lay.sv: f_ * lay.sv + lay.n_v] = w
+    h = torch.as_tensor(np.linspace(-0.3, 0.7, j)).to(ctx.device)
+    hout = ctx.h2[:j]
+    from nekstab_next_amd._lib import NKV_TIME_DOT
+    ctx.call("nkv_block_update_dot", ctx.w.data_ptr(), Q.ptr, j, h.data_ptr(), f.ptr, hout.data_ptr(),
+             ctx.ws.data_ptr(), NKV_TIME | NKV_TIME_DOT, ctx.stream)
+    fref = fh - h.cpu().numpy() @ Qh  # includes the time slot (NKV_TIME)
+    np.testing.assert_allclose(f.to_packed(), fref, rtol=1e-12, atol=1e-13)
+    t = lay.time_offset
+    href = Qh @ (wfull * fref) + Qh[:, t] * fref[t]
+    np.testing.assert_allclose(hout.cpu().numpy(), href, rtol=1e-12, atol=1e-12 * np.abs(href).max())
