@@ -51,7 +51,7 @@ extern "C" {
 #define NKV_ABI_VERSION 1
 
 /* Rows per tile: fields are padded to a multiple of this many doubles. */
-#define NKV_TILE 2048
+#define NKV_TILE 4096
 
 /* Status codes (every entry point). */
 #define NKV_OK 0

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see module d
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 
-NKV_TILE = 2048
+NKV_TILE = 4096
 NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE = 0, 1, 2, 3, 4
 NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2

@@ -20,12 +20,37 @@
 
 namespace {
 
+// Tuning knobs (compile-time; tools/tune_kernels.py builds variants and times them on MI355X):
+#ifndef NKV_PAIRS
+#define NKV_PAIRS 8  // double2 per thread per tile in the dot/update kernels (large problems)
+#endif
+#ifndef NKV_PAIRS_SMALL
+#define NKV_PAIRS_SMALL 2  // ... when the vector has fewer than NKV_SMALL_TILES large tiles
+#endif
+#ifndef NKV_SMALL_TILES
+#define NKV_SMALL_TILES 2048
+#endif
+#ifndef NKV_COLU
+#define NKV_COLU 4  // basis columns in flight per thread in the multi-dot
+#endif
+#ifndef NKV_NT
+#define NKV_NT 1  // non-temporal loads for the streamed basis columns
+#endif
+#ifndef NKV_MAXB
+#define NKV_MAXB 1024  // workgroups (= reduction partials per column) of the dot/update kernels
+#endif
+#ifndef NKV_FUSE_NW
+#define NKV_FUSE_NW 8  // waves per workgroup of the fused update+dot for j <= 16*NKV_FUSE_NW
+#endif
+#ifndef NKV_FUSE_G
+#define NKV_FUSE_G 1024  // workgroups of the fused update+dot
+#endif
+
 constexpr int kThreads = 256;                       // 4 waves of 64
-constexpr int kPairs = 4;                            // double2 per thread per tile
-constexpr int kTile = kThreads * kPairs * 2;         // 2048 rows per tile
-static_assert(kTile == NKV_TILE, "tile size must match the documented padding");
-constexpr int kMaxBlocks = 2048;                     // reduction partial slots per column
-constexpr int kColUnroll = 4;                        // columns in flight per thread (block dot)
+static_assert(NKV_TILE % (kThreads * NKV_PAIRS * 2) == 0, "kernel tile must divide the padding");
+static_assert(NKV_TILE % (kThreads * NKV_PAIRS_SMALL * 2) == 0, "kernel tile must divide the padding");
+constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots per column
+constexpr int kColUnroll = NKV_COLU;                 // columns in flight per thread (block dot)
 constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
 constexpr int kRotRows = 64;                         // rows per rotation tile
 constexpr int kRotMaxK = 256;
@@ -67,7 +92,7 @@ int check_layout(const nkv_layout* L) {
     if (L->n_wf < 1 || L->n_v < 0 || L->n_p < 0)
         return fail(NKV_EINVAL, "bad layout: n_wf=%d n_v=%lld n_p=%lld", L->n_wf,
                     (long long)L->n_v, (long long)L->n_p);
-    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % kTile || L->sp % kTile || L->ld % kTile)
+    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % NKV_TILE || L->sp % NKV_TILE || L->ld % NKV_TILE)
         return fail(NKV_ESHAPE, "layout not padded to NKV_TILE: sv=%lld sp=%lld ld=%lld",
                     (long long)L->sv, (long long)L->sp, (long long)L->ld);
     if (L->ld < rows_of(L) + 1)
@@ -110,6 +135,18 @@ __device__ __forceinline__ double block_sum(double v, double* lds4) {
 }
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+// Loads of streamed basis columns: each byte is read once per pass and, at the sizes that matter,
+// the basis is far larger than L2 + Infinity Cache, so the loads are non-temporal (NKV_NT).
+__device__ __forceinline__ double2 ldq(const double* p) {
+#if NKV_NT
+    const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+    return make_double2(v.x, v.y);
+#else
+    return ld2(p);
+#endif
+}
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
 
 // ------------------------------------------------------------------------------------------
@@ -118,11 +155,13 @@ __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<do
 // the field (no per-element division).  Each thread keeps its 8 rows of w.f in registers and
 // streams the j basis columns past them, kColUnroll columns in flight.
 // ------------------------------------------------------------------------------------------
+template <int kPairs>
 __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict__ Q, int64_t ld,
                                                         int j, const double* __restrict__ f,
                                                         const double* __restrict__ w, int64_t sv,
                                                         int tiles_per_field,
                                                         double* __restrict__ partials, int B) {
+    constexpr int kTile = kThreads * kPairs * 2;
     extern __shared__ double red[];  // [4 waves][j]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 4 * j; c += kThreads) red[c] = 0.0;
@@ -146,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
 #pragma unroll
             for (int u = 0; u < kColUnroll; ++u)
 #pragma unroll
-                for (int k = 0; k < kPairs; ++k) q[u][k] = ld2(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
             double s[kColUnroll];
 #pragma unroll
             for (int u = 0; u < kColUnroll; ++u) {
@@ -171,7 +210,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
             double a = 0.0;
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) {
-                const double2 q = ld2(qb + (int64_t)c * ld + k * 2 * kThreads);
+                const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
                 a = fma(q.x, wf[k].x, a);
                 a = fma(q.y, wf[k].y, a);
             }
@@ -208,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_cols(const double* __restri
 // 1-D grid-stride over all tiles of the vector; a tile never straddles fields (sv, sp are
 // multiples of the tile), so the weight row is r - field*sv.
 // ------------------------------------------------------------------------------------------
-template <bool OVERWRITE, bool NORM>
+template <bool OVERWRITE, bool NORM, int kPairs>
 __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restrict__ Q, int64_t ld,
                                                            int j, const double* __restrict__ h,
                                                            double* __restrict__ f,
@@ -217,6 +256,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
                                                            int tiles_total, int64_t time_off,
                                                            int do_time,
                                                            double* __restrict__ partials) {
+    constexpr int kTile = kThreads * kPairs * 2;
     __shared__ double lds4[4];
     // time slot (one double): wave 0 of block 0, lanes split the columns.
     if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
@@ -241,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int k = 0; k < kPairs; ++k) q[u][k] = ld2(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const double hc = OVERWRITE ? h[c + u] : -h[c + u];
@@ -256,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
             const double hc = OVERWRITE ? h[c] : -h[c];
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) {
-                const double2 q = ld2(qb + (int64_t)c * ld + k * 2 * kThreads);
+                const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
                 acc[k].x = fma(hc, q.x, acc[k].x);
                 acc[k].y = fma(hc, q.y, acc[k].y);
             }
@@ -298,7 +338,7 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
                                                          int64_t tiles_total, int64_t time_off,
                                                          int do_time, double* __restrict__ partials,
                                                          int B) {
-    __shared__ double2 part[NW][64];
+    __shared__ double2 part[2][NW][64];  // double-buffered: one barrier per tile
     // wave index made provably uniform: column bases become scalar registers, the per-lane part of
     // every address is one 32-bit row offset
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -320,11 +360,14 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
     double acc[CPW];
 #pragma unroll
     for (int i = 0; i < CPW; ++i) acc[i] = 0.0;
-    for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+    int buf = 0;
+    for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x, buf ^= 1) {
         const uint32_t r = (uint32_t)(t * kFuseRows) + 2u * lane;
         double2 q[CPW];
 #pragma unroll
-        for (int i = 0; i < CPW; ++i) q[i] = ld2(qcol[i] + r);
+        for (int i = 0; i < CPW - 1; ++i) q[i] = ldq(qcol[i] + r);
+        // CPW = ceil(j/NW): only the last slot can lie past j (wave-uniform test, never fetched)
+        q[CPW - 1] = (wv + NW * (CPW - 1) < j) ? ldq(qcol[CPW - 1] + r) : make_double2(0.0, 0.0);
         double2 s = make_double2(0.0, 0.0);
 #pragma unroll
         for (int i = 0; i < CPW; ++i) {
@@ -332,12 +375,12 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
             s.y = fma(hc[i], q[i].y, s.y);
         }
         const double2 fv = ld2(f + r);
-        part[wv][lane] = s;
+        part[buf][wv][lane] = s;
         __syncthreads();
-        double2 tot = part[0][lane];
+        double2 tot = part[buf][0][lane];
 #pragma unroll
         for (int k = 1; k < NW; ++k) {
-            const double2 p = part[k][lane];
+            const double2 p = part[buf][k][lane];
             tot.x += p.x;
             tot.y += p.y;
         }
@@ -350,7 +393,8 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 #pragma unroll
             for (int i = 0; i < CPW; ++i) acc[i] = fma(q[i].y, b, fma(q[i].x, a, acc[i]));
         }
-        __syncthreads();
+        // no second barrier: the next tile writes the other buffer, and a wave can only reach the
+        // barrier after it once every wave has passed this tile's barrier (and read this buffer)
     }
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
@@ -603,9 +647,15 @@ inline double* partials_of(void* ws) {
     return reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + kCtrlBytes);
 }
 
-// Shared launcher for block dots (nkv_dot is the j = 1 case).
-int launch_block_dot(const nkv_layout* L, const double* w, const double* Q, int64_t ld, int j,
-                     const double* f, double* out, void* ws, unsigned flags, hipStream_t st) {
+// Rows per thread: NKV_PAIRS*2 when the vector has enough large tiles to fill the chip, else fewer.
+inline bool use_large_tiles(const nkv_layout* L) {
+    return rows_of(L) / (kThreads * NKV_PAIRS * 2) >= NKV_SMALL_TILES;
+}
+
+template <int P>
+int launch_block_dot_p(const nkv_layout* L, const double* w, const double* Q, int64_t ld, int j,
+                       const double* f, double* out, void* ws, unsigned flags, hipStream_t st) {
+    constexpr int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
     int bx = kMaxBlocks / L->n_wf;
     if (bx > tpf) bx = tpf;
@@ -613,7 +663,7 @@ int launch_block_dot(const nkv_layout* L, const double* w, const double* Q, int6
     const int B = bx * L->n_wf;
     double* part = partials_of(ws);
     if (tpf > 0) {
-        hipLaunchKernelGGL(k_block_dot, dim3(bx, L->n_wf), dim3(kThreads), 4 * j * sizeof(double), st,
+        hipLaunchKernelGGL(k_block_dot<P>, dim3(bx, L->n_wf), dim3(kThreads), 4 * j * sizeof(double), st,
                            Q, ld, j, f, w, L->sv, tpf, part, B);
         NKV_LAUNCHED();
     }
@@ -621,6 +671,39 @@ int launch_block_dot(const nkv_layout* L, const double* w, const double* Q, int6
     const bool tdot = (flags & NKV_TIME) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, out,
                        tdot ? Q + T : nullptr, ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+// Shared launcher for block dots (nkv_dot is the j = 1 case).
+int launch_block_dot(const nkv_layout* L, const double* w, const double* Q, int64_t ld, int j,
+                     const double* f, double* out, void* ws, unsigned flags, hipStream_t st) {
+    return use_large_tiles(L) ? launch_block_dot_p<NKV_PAIRS>(L, w, Q, ld, j, f, out, ws, flags, st)
+                              : launch_block_dot_p<NKV_PAIRS_SMALL>(L, w, Q, ld, j, f, out, ws, flags, st);
+}
+
+template <int P>
+int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q, int j, const double* h_dev,
+                          double* f, double* part, unsigned flags, hipStream_t st, int* g_out) {
+    constexpr int kTile = kThreads * P * 2;
+    const bool over = (flags & NKV_OVERWRITE) != 0;
+    const bool norm = (flags & NKV_NORM2) != 0;
+    const int tpf = (int)(L->sv / kTile);
+    const int tiles_w = tpf * L->n_wf;
+    const int tiles_total = (int)(rows_of(L) / kTile);
+    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    if (g < 1) g = 1;
+    *g_out = g;
+    const int64_t T = rows_of(L);
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    if (over && norm)
+        hipLaunchKernelGGL((k_block_update<true, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else if (over)
+        hipLaunchKernelGGL((k_block_update<true, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else if (norm)
+        hipLaunchKernelGGL((k_block_update<false, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else
+        hipLaunchKernelGGL((k_block_update<false, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -760,31 +843,18 @@ int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int 
     CHECK(check_ptr(f, "f"));
     if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
     if (j < 0) return fail(NKV_EINVAL, "j=%d < 0", j);
-    const bool over = (flags & NKV_OVERWRITE) != 0;
     const bool norm = (flags & NKV_NORM2) != 0;
     if (norm) {
         CHECK(check_ptr(w, "w"));
         CHECK(check_ptr(ws, "ws"));
         if (!nrm2_dev) return fail(NKV_EINVAL, "nrm2_dev is NULL");
     }
-    const int tpf = (int)(L->sv / kTile);
-    const int tiles_w = tpf * L->n_wf;
-    const int tiles_total = (int)(rows_of(L) / kTile);
-    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
-    if (g < 1) g = 1;
-    const int64_t T = rows_of(L);
-    const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = ws ? partials_of(ws) : nullptr;
     hipStream_t st = S(stream);
-    if (over && norm)
-        hipLaunchKernelGGL((k_block_update<true, true>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (over)
-        hipLaunchKernelGGL((k_block_update<true, false>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (norm)
-        hipLaunchKernelGGL((k_block_update<false, true>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else
-        hipLaunchKernelGGL((k_block_update<false, false>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    NKV_LAUNCHED();
+    int g = 1;
+    const int64_t T = rows_of(L);
+    if (use_large_tiles(L)) CHECK(launch_block_update_p<NKV_PAIRS>(L, w, Q, j, h_dev, f, part, flags, st, &g));
+    else CHECK(launch_block_update_p<NKV_PAIRS_SMALL>(L, w, Q, j, h_dev, f, part, flags, st, &g));
     if (norm) {
         // ||f||^2 time term: (uparam(1)==2.1 / real_dot) only on the rank owning the replicated scalar
         const bool tdot = (flags & NKV_TIME) && L->rank0;
@@ -814,7 +884,7 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     const int64_t tiles_total = rows / kFuseRows;
     const int64_t tpf = L->sv / kFuseRows;
     const int64_t tiles_w = tpf * L->n_wf;
-    int64_t g = tiles_total < 1024 ? tiles_total : 1024;
+    int64_t g = tiles_total < NKV_FUSE_G ? tiles_total : NKV_FUSE_G;
     if (g < 1) g = 1;
     const int B = (int)g;
     const int64_t T = rows;
@@ -824,12 +894,39 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
 #define NKV_FUSE(NW, CPW)                                                                                     \
     hipLaunchKernelGGL((k_update_dot<NW, CPW>), dim3((unsigned)g), dim3(NW * 64), 0, st, Q, L->ld, j, h_dev, f, w, \
                        L->sv, tpf, tiles_w, tiles_total, T, dt, part, B)
-    if (j <= 8) NKV_FUSE(8, 1);
-    else if (j <= 16) NKV_FUSE(8, 2);
-    else if (j <= 32) NKV_FUSE(8, 4);
-    else if (j <= 64) NKV_FUSE(8, 8);
-    else if (j <= 128) NKV_FUSE(8, 16);
-    else NKV_FUSE(16, 16);
+    constexpr int NW = NKV_FUSE_NW;
+    const int cpw = j <= NW * 16 ? (j + NW - 1) / NW : (j + 15) / 16;
+    if (j <= NW * 16) {
+        switch (cpw) {
+            case 1: NKV_FUSE(NW, 1); break;
+            case 2: NKV_FUSE(NW, 2); break;
+            case 3: NKV_FUSE(NW, 3); break;
+            case 4: NKV_FUSE(NW, 4); break;
+            case 5: NKV_FUSE(NW, 5); break;
+            case 6: NKV_FUSE(NW, 6); break;
+            case 7: NKV_FUSE(NW, 7); break;
+            case 8: NKV_FUSE(NW, 8); break;
+            case 9: NKV_FUSE(NW, 9); break;
+            case 10: NKV_FUSE(NW, 10); break;
+            case 11: NKV_FUSE(NW, 11); break;
+            case 12: NKV_FUSE(NW, 12); break;
+            case 13: NKV_FUSE(NW, 13); break;
+            case 14: NKV_FUSE(NW, 14); break;
+            case 15: NKV_FUSE(NW, 15); break;
+            default: NKV_FUSE(NW, 16); break;
+        }
+    } else {  // 16 waves, up to 16 columns each (j <= 256)
+        switch (cpw) {
+            case 9: NKV_FUSE(16, 9); break;
+            case 10: NKV_FUSE(16, 10); break;
+            case 11: NKV_FUSE(16, 11); break;
+            case 12: NKV_FUSE(16, 12); break;
+            case 13: NKV_FUSE(16, 13); break;
+            case 14: NKV_FUSE(16, 14); break;
+            case 15: NKV_FUSE(16, 15); break;
+            default: NKV_FUSE(16, 16); break;
+        }
+    }
 #undef NKV_FUSE
     NKV_LAUNCHED();
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
-NKV_TILE = 2048  # include/nekkrylov.h
+NKV_TILE = 4096  # include/nekkrylov.h
 
 
 def _roundup(n: int, m: int) -> int:

@@ -1,0 +1,138 @@
+#!/usr/bin/env python
+"""Build compile-time variants of libnekkrylov (tile rows, columns in flight, non-temporal loads,
+grid size) and time the Gram–Schmidt entry points at BASELINE size in ONE process, interleaved
+over rounds (cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/tune_kernels.py build            # here (hipcc cross-compiles)
+  python tools/tune_kernels.py run [--E 44176]  # on the MI355X box
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "tools", "variants")
+
+VARIANTS = {
+    "base": {},
+    "nt": {"NKV_NT": 1},
+    "pairs2": {"NKV_PAIRS": 2},
+    "pairs8": {"NKV_PAIRS": 8},
+    "colu2": {"NKV_COLU": 2},
+    "colu8": {"NKV_COLU": 8},
+    "maxb1024": {"NKV_MAXB": 1024},
+    "maxb4096": {"NKV_MAXB": 4096},
+    "nt_pairs8": {"NKV_NT": 1, "NKV_PAIRS": 8},
+    "nt_p8_b1024": {"NKV_NT": 1, "NKV_PAIRS": 8, "NKV_MAXB": 1024},
+    "nt_p8_c2": {"NKV_NT": 1, "NKV_PAIRS": 8, "NKV_COLU": 2},
+    "nt_p4_c8_b1024": {"NKV_NT": 1, "NKV_COLU": 8, "NKV_MAXB": 1024},
+    "nt_f16": {"NKV_NT": 1, "NKV_FUSE_NW": 16},
+    "nt_fg512": {"NKV_NT": 1, "NKV_FUSE_G": 512},
+    "nt_fg2048": {"NKV_NT": 1, "NKV_FUSE_G": 2048},
+    "nt_f16_g512": {"NKV_NT": 1, "NKV_FUSE_NW": 16, "NKV_FUSE_G": 512},
+}
+
+
+def build(names):
+    os.makedirs(VDIR, exist_ok=True)
+    src = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
+    procs = []
+    for n in names:
+        defs = [f"-D{k}={v}" for k, v in VARIANTS[n].items()]
+        out = os.path.join(VDIR, f"lib_{n}.so")
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I" + os.path.join(ROOT, "include"), *defs, src, "-o", out]
+        procs.append(subprocess.Popen(cmd))
+    for p in procs:
+        assert p.wait() == 0
+
+
+def run(names, E, rounds, js):
+    import numpy as np
+    import torch
+
+    from nekstab_next_amd import _lib
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import box3d_layout
+
+    libs = {}
+    for n in names:
+        L = ctypes.CDLL(os.path.join(VDIR, f"lib_{n}.so"))
+        for name, (res, args) in _lib._SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        libs[n] = L
+    lay = box3d_layout(E)
+    jmax = max(js)
+    dev = torch.device("cuda", 0)
+    Lc = lay.c_struct()
+    Lp = ctypes.byref(Lc)
+    Q = torch.empty((jmax + 1, lay.ld), dtype=torch.float64, device=dev)
+    lib0 = libs[names[0]]
+    st = torch.cuda.current_stream().cuda_stream
+    for i in range(jmax + 1):
+        _lib.check(lib0.nkv_fill_hash(Lp, Q[i].data_ptr(), 100 + i, 0, 0, st), "fill")
+    f = torch.empty(lay.ld, dtype=torch.float64, device=dev)
+    _lib.check(lib0.nkv_fill_hash(Lp, f.data_ptr(), 5, 0, 0, st), "fill")
+    w = torch.zeros(lay.sv, dtype=torch.float64, device=dev)
+    w[: lay.n_v] = torch.as_tensor(syn.mass_weights(lay)).to(dev)
+    ws = torch.zeros((lib0.nkv_workspace_bytes(Lp, jmax + 1) + 7) // 8 + 4096 * (jmax + 2), dtype=torch.float64, device=dev)
+    h = torch.full((jmax + 1,), 1e-3, dtype=torch.float64, device=dev)
+    h2 = torch.zeros(jmax + 1, dtype=torch.float64, device=dev)
+    nrm = torch.zeros(8, dtype=torch.float64, device=dev)
+    N, Nw, nv = lay.N, lay.N_w, lay.n_v
+
+    def ops(L, j):
+        return {
+            "dot": (lambda: L.nkv_block_dot(Lp, w.data_ptr(), Q.data_ptr(), j, f.data_ptr(), h2.data_ptr(), ws.data_ptr(), 0, st),
+                    8.0 * (j * Nw + Nw + nv)),
+            "update_norm": (lambda: L.nkv_block_update(Lp, w.data_ptr(), Q.data_ptr(), j, h.data_ptr(), f.data_ptr(), nrm.data_ptr(), ws.data_ptr(), 0x1 | 0x8, st),
+                            8.0 * (j * N + 2 * N + nv)),
+            "update_dot": (lambda: L.nkv_block_update_dot(Lp, w.data_ptr(), Q.data_ptr(), j, h.data_ptr(), f.data_ptr(), h2.data_ptr(), ws.data_ptr(), 0x1, st),
+                           8.0 * (j * N + 2 * N + nv)),
+        }
+
+    res = {}
+    for r in range(rounds):
+        for n in names:
+            for j in js:
+                for opname, (fn, nbytes) in ops(libs[n], j).items():
+                    fn()  # warm
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    reps = 3
+                    for _ in range(reps):
+                        rc = fn()
+                        assert rc == 0, (n, opname, rc)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / reps
+                    res.setdefault((n, j, opname), []).append(nbytes / (ms * 1e-3) / 1e9)
+    out = {}
+    for (n, j, op), v in sorted(res.items()):
+        out[f"{n} j={j} {op}"] = dict(median_gbs=float(np.median(v)), min_gbs=float(np.min(v)), max_gbs=float(np.max(v)))
+        print(f"{n:10s} j={j:4d} {op:12s} median {np.median(v):8.1f} GB/s  (min {np.min(v):.1f})", flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--E", type=int, default=44176)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--js", default="32,128")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tune.json"))
+    a = ap.parse_args()
+    names = a.variants.split(",")
+    if a.cmd == "build":
+        build(names)
+    else:
+        out = run(names, a.E, a.rounds, [int(x) for x in a.js.split(",")])
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        json.dump(out, open(a.out, "w"), indent=1)
