@@ -1,0 +1,33 @@
+#!/usr/bin/env python
+"""Compare rocprofv3 --stats per-kernel-family average durations with bench.py's live HIP-event
+phase timings (the bench's `roofline.avg_launch_ms` must agree with the profiler).
+
+usage: tools/check_profile.py KERNEL_STATS_CSV BENCH_JSON
+"""
+import csv
+import json
+import sys
+
+FAM = {"block_dot": "k_block_dot", "update_dot": "k_update_dot", "block_update": "k_block_update<false, true",
+       "finish": "k_finish", "op_diag": "k_op_diag"}
+
+
+def main():
+    stats = list(csv.DictReader(open(sys.argv[1])))
+    bench = json.load(open(sys.argv[2]))
+    print(f"{'family':14s} {'rocprof calls':>13s} {'rocprof avg ms':>15s} {'events launches':>16s} {'events avg ms':>14s} {'ratio':>7s}")
+    for fam, key in FAM.items():
+        rows = [r for r in stats if key in r["Name"]]
+        if not rows:
+            continue
+        calls = sum(int(r["Calls"]) for r in rows)
+        tot = sum(float(r["TotalDurationNs"]) for r in rows)
+        ph = bench.get("phases", {}).get(fam)
+        ev = f"{ph['launches']:16d} {ph['avg_ms']:14.4f} {ph['avg_ms'] / (tot / calls / 1e6):7.3f}" if ph else ""
+        print(f"{fam:14s} {calls:13d} {tot / calls / 1e6:15.4f} {ev}")
+    print("(rocprof counts every launch incl. warm-up and the j=1 seed dots; events cover the timed steps; "
+          "event brackets include the ~5 us second-stage reduction kernel)")
+
+
+if __name__ == "__main__":
+    main()
