@@ -133,11 +133,11 @@ def main():
     from nekstab_next_amd.profiling import PhaseTimer
     from nekstab_next_amd.vector import NekContext
 
-    comm = init_from_env("nccl")
+    comm = init_from_env(os.environ.get("NKV_BACKEND", "nccl"))
     rank, world = comm.rank, comm.world
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -60,6 +60,8 @@ def init_from_env(backend: str | None = None) -> Comm:
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
-        else:
+        else:  # gloo: CPU tests, or several ranks sharing one GPU (rehearsal of the sharded path)
+            if torch.cuda.is_available():
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
             dist.init_process_group(backend)
     return Comm()

@@ -1,0 +1,88 @@
+"""Sharded (world_size 2) GPU path on ONE MI355X: two ranks share the device and exchange partial
+dots through gloo (RCCL cannot place two ranks on one GPU; on an 8-GPU node the same code runs over
+RCCL/xGMI).  Sharded Krylov–Schur must reproduce the single-rank result: identical restart
+trajectory, Ritz values to 1e-12 (SURVEY.md §8(e) gate)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ks(world_rank_pair, out, port):
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import KrylovSchurConfig
+        from nekstab_next_amd.krylov_schur import krylov_schur
+        from nekstab_next_amd.layout import box3d_layout, cylinder_layout
+        from nekstab_next_amd.operators import DiagOperator, Rot2Operator
+        from nekstab_next_amd.vector import NekContext
+
+        res = {}
+        comm = Comm()
+        lay = box3d_layout(96).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=comm, max_cols=48)
+        d, _ = syn.laplacian_shift_invert(lay)
+        seed = ctx.vector()
+        seed.fill_hash(11)
+        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4))
+        res["lap"] = (r.vals, r.residual, r.mstart_history, r.schur_cnt, r.H)
+        lay2 = cylinder_layout(400).shard(rank, world)
+        ctx2 = NekContext(lay2, weights=syn.mass_weights(lay2), comm=comm, max_cols=48)
+        c, s, dr, _ = syn.rot2_operator(lay2)
+        seed2 = ctx2.vector()
+        seed2.fill_hash(5)
+        r2 = krylov_schur(ctx2, Rot2Operator(ctx2, c, s, dr), seed2, KrylovSchurConfig(k_dim=24, schur_tgt=2))
+        res["rot"] = (r2.vals, r2.residual, r2.mstart_history, r2.schur_cnt, r2.H)
+        out[(world, rank)] = res
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_two_ranks_match_one_rank(gpu):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_ks, args=((0, 1), out, _free_port()))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    port = _free_port()
+    procs = [ctx.Process(target=_run_ks, args=((r, 2), out, port)) for r in range(2)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    for key in ("lap", "rot"):
+        v1, r1, m1, c1, H1 = out[(1, 0)][key]
+        for rank in range(2):
+            v2, r2, m2, c2, H2 = out[(2, rank)][key]
+            assert m2 == m1 and c2 == c1
+            conv = r1 < 1e-6
+            sel = np.nonzero(conv)[0].tolist() + list(range(8))
+            sel = sorted(set(sel))
+            assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) < 1e-12
+        np.testing.assert_array_equal(out[(2, 0)][key][4], out[(2, 1)][key][4])  # identical H on ranks
