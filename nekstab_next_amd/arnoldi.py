@@ -58,7 +58,22 @@ def update_hessenberg_matrix(ctx: NekContext, Q: Basis, k: int, f: NekVector, Hd
     j = int(k)
     if j + 1 > Q.k or j > ctx.max_cols:
         raise ValueError(f"step {j} exceeds basis size {Q.k} / max_cols {ctx.max_cols}")
+    orthonormalize(ctx, Q, j, f, Q.col_ptr(j), Hd.col_ptr(j - 1), mode)
+
+
+def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int, hcol_ptr: int,
+                   mode: str = "cgs2") -> None:
+    """Two-pass Gram–Schmidt of f against Q[0:j] (W inner product), then out = f/||f||; the
+    projection coefficients h1+h2 go to hcol[0:j] and ||f|| to hcol[j] (device memory).  j = 0
+    only normalises."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    if j == 0:
+        tf = NKV_TIME if ctx.time_in_dot else 0
+        nrm = ctx.scal[3:4]
+        ctx.call("nkv_dot", w, f.ptr, f.ptr, nrm.data_ptr(), ws, tf, st)
+        ctx.comm.allreduce_(nrm)
+        ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), out_ptr, 0, ctx.h1.data_ptr(), None, hcol_ptr, 0, st)
+        return
     tf = NKV_TIME if ctx.time_in_dot else 0
     h1, h2, nrm = ctx.h1[:j], ctx.h2[:j], ctx.scal[3:4]
     if mode in ("cgs2", "cgs2-unfused"):
@@ -111,8 +126,8 @@ def update_hessenberg_matrix(ctx: NekContext, Q: Basis, k: int, f: NekVector, Hd
         raise ValueError(f"unknown orthogonalisation mode {mode!r}")
     if ctx.timer:
         ctx.timer.begin("finish")
-    ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), Q.col_ptr(j), j, h1.data_ptr(), h2.data_ptr(),
-             Hd.col_ptr(j - 1), 0, st)
+    ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), out_ptr, j, h1.data_ptr(), h2.data_ptr(),
+             hcol_ptr, 0, st)
     if ctx.timer:
         ctx.timer.end("finish", 16.0 * ctx.layout.N)
 

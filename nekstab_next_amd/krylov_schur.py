@@ -73,16 +73,27 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
 
 
 def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: KrylovSchurConfig | None = None,
-                 transpose: bool = False, on_restart=None) -> KrylovSchurResult:
+                 transpose: bool = False, on_restart=None, Q: Basis | None = None, on_step=None,
+                 start=None) -> KrylovSchurResult:
     """Eigenpairs of ``op`` of largest modulus by Krylov–Schur restarts (reference defaults from
-    core/main.f90:9-12: k_dim=100, schur_tgt=2, eigen_tol=1e-6, schur_del=0.1)."""
+    core/main.f90:9-12: k_dim=100, schur_tgt=2, eigen_tol=1e-6, schur_del=0.1).
+
+    ``Q``: caller-owned basis of k_dim+1 vectors (LightKrylov's ``X``), else allocated.
+    ``on_step(mstep, Q, Hd)``: per-Arnoldi-step hook (checkpointing, ifres).
+    ``start=(mstart, H)``: resume from a checkpoint (Q[0:mstart] already loaded, uparam(2) > 0,
+    eigensolvers.f90:240-285); ``seed`` is then ignored."""
     cfg = cfg or KrylovSchurConfig()
     k = cfg.k_dim
-    Q = ctx.basis(k + 1)
+    if Q is None:
+        Q = ctx.basis(k + 1)
+    elif Q.k < k + 1:
+        raise ValueError(f"basis has {Q.k} vectors, k_dim+1={k + 1} needed")
     Hd = HessenbergDev(ctx, k)
     H = np.zeros((k + 1, k), order="F")
     f = ctx.vector()
-    if cfg.seed_mode == "normalize":
+    if start is not None:
+        pass
+    elif cfg.seed_mode == "normalize":
         prepare_seed(seed, Q[0])
     elif cfg.seed_mode == "noise":
         # ifseed_nois branch of the in-tree driver: Q(1) = A (seed/||seed||), NOT renormalised
@@ -98,10 +109,16 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         raise ValueError(cfg.seed_mode)
 
     mstart = 1
+    if start is not None:
+        mstart, H0 = start
+        H[...] = H0
+        Hd.upload(H)
+        mstart = int(mstart) + 1  # "careful here!" (eigensolvers.f90:281)
     schur_cnt = 0
     res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
+    hook = None if on_step is None else (lambda mstep: on_step(mstep, Q, Hd))
     while True:
-        arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose)
+        arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook)
         H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
         ctx.check_nan()
         vals, vecs = lapack.eig(H[:k, :k])
