@@ -1,0 +1,242 @@
+"""Nek5000 field files (``#std`` ``.f#####``) <-> nekStab state vectors.
+
+nekStab reads base flows and restart vectors with Nek5000's ``load_fld`` (core/IO.f90:12-73,
+eigensolvers.f90:170-180) and writes Krylov vectors / eigenmodes with ``outpost2``
+(eigensolvers.f90:236,607-615,776).  The on-disk format, as found in the reference's own data
+(``examples/cylinder/BF_1cyl0.f00001``):
+
+* 132-byte ASCII header: ``#std <wdsize> <nx> <ny> <nz> <nel_in_file> <nelgt> <time> <istep>
+  <fid0> <nfileo> <rdcode>`` (rdcode letters: X coordinates, U velocity, P pressure, T
+  temperature, S<nn> passive scalars);
+* float32 endian tag 6.54321;
+* int32 global element ids (1-based) of the elements in this file, in file order;
+* per field group, element after element: vector groups (X, U) write their ldim components
+  component-major inside each element, scalar groups one block per element.
+  Pressure is stored on the velocity (GLL, lx1) mesh; in memory PN/PN-2 pressure lives on the
+  Gauss–Legendre lx2 mesh, so it is interpolated on read (lx1 GLL -> lx2 GL) and on write.
+
+Multi-rank: each rank writes its element range as file ``fid = rank`` with ``nfileo = world``
+(Nek5000's multi-file naming ``<prefix><session><fid>.f<NNNNN>``).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .layout import NekLayout
+from .synthetic import gll_weights  # noqa: F401  (shared GLL quadrature helpers)
+
+ENDIAN_TAG = np.float32(6.54321)
+
+
+# ---- 1-D nodes and interpolation (pressure mesh mapping) ------------------------------------
+
+def gll_points(n: int) -> np.ndarray:
+    P = np.polynomial.legendre.Legendre.basis(n - 1)
+    return np.concatenate([[-1.0], np.sort(P.deriv().roots().real), [1.0]])
+
+
+def gauss_points(n: int) -> np.ndarray:
+    return np.polynomial.legendre.leggauss(n)[0]
+
+
+def interp_matrix(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """Lagrange interpolation from nodes ``src`` to points ``dst`` (len(dst) x len(src))."""
+    M = np.ones((len(dst), len(src)))
+    for j, xj in enumerate(src):
+        for m, xm in enumerate(src):
+            if m != j:
+                M[:, j] *= (dst - xm) / (xj - xm)
+    return M
+
+
+def _tensor_apply(M: np.ndarray, data: np.ndarray, ldim: int) -> np.ndarray:
+    """Apply the 1-D operator M along every direction of per-element data [nel, n^ldim] (x fastest)."""
+    nel = data.shape[0]
+    n = M.shape[1]
+    if ldim == 2:
+        a = data.reshape(nel, n, n)  # [e, y, x]
+        return np.einsum("ix,jy,eyx->eji", M, M, a).reshape(nel, -1)
+    a = data.reshape(nel, n, n, n)  # [e, z, y, x]
+    return np.einsum("ix,jy,kz,ezyx->ekji", M, M, M, a).reshape(nel, -1)
+
+
+def map_pressure_to_mesh1(p2: np.ndarray, lx1: int, lx2: int, ldim: int) -> np.ndarray:
+    if lx1 == lx2:
+        return p2
+    return _tensor_apply(interp_matrix(gauss_points(lx2), gll_points(lx1)), p2, ldim)
+
+
+def map_pressure_to_mesh2(p1: np.ndarray, lx1: int, lx2: int, ldim: int) -> np.ndarray:
+    if lx1 == lx2:
+        return p1
+    return _tensor_apply(interp_matrix(gll_points(lx1), gauss_points(lx2)), p1, ldim)
+
+
+# ---- file I/O --------------------------------------------------------------------------------
+
+@dataclass
+class FldFile:
+    nx: int
+    ny: int
+    nz: int
+    nelgt: int
+    time: float = 0.0
+    istep: int = 0
+    fid0: int = 0
+    nfileo: int = 1
+    rdcode: str = "UP"
+    emap: np.ndarray = None            # 1-based global element ids of the elements in the file
+    fields: dict = field(default_factory=dict)  # name -> [nel, pts]: x,y,z, vx,vy,vz, pr, t, s01..
+    wdsize: int = 8
+
+    @property
+    def ldim(self) -> int:
+        return 3 if self.nz > 1 else 2
+
+
+def _groups(rdcode: str):
+    out, i = [], 0
+    while i < len(rdcode):
+        c = rdcode[i]
+        if c == "S":
+            out.append(rdcode[i:i + 3])
+            i += 3
+        else:
+            out.append(c)
+            i += 1
+    return out
+
+
+def read_fld(path: str) -> FldFile:
+    raw = open(path, "rb").read()
+    hdr = raw[:132].decode("ascii", errors="replace")
+    tok = hdr.split()
+    if tok[0] != "#std":
+        raise ValueError(f"{path}: not a Nek5000 #std field file")
+    wdsize, nx, ny, nz, nel, nelgt = (int(t) for t in tok[1:7])
+    time, istep, fid0, nfileo = float(tok[7]), int(tok[8]), int(tok[9]), int(tok[10])
+    rdcode = tok[11]
+    tag = np.frombuffer(raw[132:136], "<f4")[0]
+    order = "<" if abs(tag - ENDIAN_TAG) < 1e-5 else ">"
+    emap = np.frombuffer(raw[136:136 + 4 * nel], order + "i4").copy()
+    fdt = np.dtype(order + ("f8" if wdsize == 8 else "f4"))
+    data = np.frombuffer(raw[136 + 4 * nel:], fdt).astype(np.float64)
+    pts = nx * ny * nz
+    ldim = 3 if nz > 1 else 2
+    f = FldFile(nx, ny, nz, nelgt, time, istep, fid0, nfileo, rdcode, emap, {}, wdsize)
+    o = 0
+    for g in _groups(rdcode):
+        if g in ("X", "U"):
+            blk = data[o:o + nel * ldim * pts].reshape(nel, ldim, pts)
+            o += nel * ldim * pts
+            names = ["x", "y", "z"] if g == "X" else ["vx", "vy", "vz"]
+            for c in range(ldim):
+                f.fields[names[c]] = blk[:, c, :].copy()
+        else:
+            blk = data[o:o + nel * pts].reshape(nel, pts)
+            o += nel * pts
+            f.fields[{"P": "pr", "T": "t"}.get(g, g.lower())] = blk.copy()
+    if o != data.size:
+        raise ValueError(f"{path}: {data.size - o} trailing values (rdcode {rdcode})")
+    return f
+
+
+def write_fld(path: str, f: FldFile) -> None:
+    nel = f.emap.size
+    ldim = f.ldim
+    pts = f.nx * f.ny * f.nz
+    hdr = (f"#std {f.wdsize:1d} {f.nx:2d} {f.ny:2d} {f.nz:2d} {nel:10d} {f.nelgt:10d} {f.time:20.13E} "
+           f"{f.istep:9d} {f.fid0:6d} {f.nfileo:6d} {f.rdcode}")
+    hdr = hdr.ljust(132)[:132].encode("ascii")
+    parts = [hdr, ENDIAN_TAG.astype("<f4").tobytes(), np.asarray(f.emap, "<i4").tobytes()]
+    for g in _groups(f.rdcode):
+        if g in ("X", "U"):
+            names = ["x", "y", "z"] if g == "X" else ["vx", "vy", "vz"]
+            blk = np.stack([f.fields[names[c]] for c in range(ldim)], axis=1)
+            parts.append(np.ascontiguousarray(blk, "<f8").tobytes())
+        else:
+            parts.append(np.ascontiguousarray(f.fields[{"P": "pr", "T": "t"}.get(g, g.lower())], "<f8").tobytes())
+    with open(path, "wb") as fh:
+        for p in parts:
+            fh.write(p)
+
+
+def fld_name(prefix: str, session: str, fid: int, num: int) -> str:
+    return f"{prefix}{session}{fid}.f{num:05d}"
+
+
+# ---- vector <-> fields -----------------------------------------------------------------------
+
+def vector_from_fld(lay: NekLayout, files) -> np.ndarray:
+    """Padded host vector (this rank's shard of ``lay``) from one or several (multi-file) field files.
+    Velocity -> vx, vy, [vz]; T -> first scalar; S01.. -> next scalars; P -> pressure (mapped to
+    the lx2 Gauss mesh).  Missing fields stay zero (as load_fld leaves them untouched)."""
+    if isinstance(files, FldFile):
+        files = [files]
+    out = np.zeros(lay.ld)
+    e0, e1 = lay.elem_range()
+    names = ["vx", "vy", "vz"][: lay.ldim] + (["t"] + [f"s{i:02d}" for i in range(1, lay.n_scalars)])[: lay.n_scalars]
+    for f in files:
+        if f.nx != lay.lx1 or f.ldim != lay.ldim:
+            raise ValueError(f"field file is lx1={f.nx} ldim={f.ldim}, layout lx1={lay.lx1} ldim={lay.ldim}")
+        g = f.emap.astype(np.int64) - 1
+        sel = np.nonzero((g >= e0) & (g < e1))[0]
+        if sel.size == 0:
+            continue
+        loc = g[sel] - e0
+        for k, nm in enumerate(names):
+            if nm in f.fields:
+                seg = out[k * lay.sv: k * lay.sv + lay.n_v].reshape(lay.nelv, lay.pts_v)
+                seg[loc] = f.fields[nm][sel]
+        if "pr" in f.fields and lay.n_p:
+            p2 = map_pressure_to_mesh2(f.fields["pr"][sel], lay.lx1, lay.lx2, lay.ldim)
+            seg = out[lay.n_wf * lay.sv: lay.n_wf * lay.sv + lay.n_p].reshape(lay.nelv, lay.pts_p)
+            seg[loc] = p2
+    return out
+
+
+def fld_from_vector(lay: NekLayout, vec: np.ndarray, time: float = 0.0, istep: int = 0,
+                    coords: dict | None = None) -> FldFile:
+    """This rank's shard as a field file (fid = rank, nfileo = world)."""
+    e0, e1 = lay.elem_range()
+    f = FldFile(lay.lx1, lay.lx1, lay.lx1 if lay.ldim == 3 else 1, lay.nelgv, time, istep, lay.rank, lay.world,
+                "", np.arange(e0 + 1, e1 + 1, dtype=np.int32), {})
+    code = ""
+    if coords:
+        code += "X"
+        f.fields.update({k: np.asarray(v).reshape(lay.nelv, lay.pts_v) for k, v in coords.items()})
+    code += "U"
+    for k, nm in enumerate(["vx", "vy", "vz"][: lay.ldim]):
+        f.fields[nm] = vec[k * lay.sv: k * lay.sv + lay.n_v].reshape(lay.nelv, lay.pts_v).copy()
+    if lay.n_p:
+        code += "P"
+        p2 = vec[lay.n_wf * lay.sv: lay.n_wf * lay.sv + lay.n_p].reshape(lay.nelv, lay.pts_p)
+        f.fields["pr"] = map_pressure_to_mesh1(p2, lay.lx1, lay.lx2, lay.ldim)
+    for s in range(lay.n_scalars):
+        k = lay.ldim + s
+        nm = "t" if s == 0 else f"s{s:02d}"
+        code += "T" if s == 0 else f"S{s:02d}"
+        f.fields[nm] = vec[k * lay.sv: k * lay.sv + lay.n_v].reshape(lay.nelv, lay.pts_v).copy()
+    f.rdcode = code
+    return f
+
+
+def read_fld_set(directory: str, prefix: str, session: str, num: int) -> list:
+    """All files of a (possibly multi-file) output number."""
+    out = []
+    fid = 0
+    while True:
+        p = os.path.join(directory, fld_name(prefix, session, fid, num))
+        if not os.path.exists(p):
+            break
+        f = read_fld(p)
+        out.append(f)
+        fid += 1
+        if fid >= f.nfileo:
+            break
+    if not out:
+        raise FileNotFoundError(os.path.join(directory, fld_name(prefix, session, 0, num)))
+    return out
