@@ -1,0 +1,111 @@
+"""BoostConv residual-subspace acceleration on the device.
+
+Reference: ``BoostConv`` / ``boostconv_core`` / ``qr_dec`` / ``linear_system``
+(core/fixedp.f90:218-403).  Every ``bst_skp`` time steps the velocity residual
+r_b = v - v_old is replaced by the least-squares-corrected one using two rotating subspaces of
+``bst_snp`` columns (differences of residuals Y and of corrected residuals X):
+
+    first call:  Y(:,1) = X(:,1) = r_b;  D = 1 (all ones);  rot = 1                :294-297
+    otherwise :  Y(:,rot) -= r_b;  X(:,rot) -= Y(:,rot)                              :301-302
+                 (Q, D) = qr_dec(Y)      single-pass MGS, columns with ||.||^2 < 1e-60 set to 0
+                                          and D(j,j) = 1                              :331-385
+                 c = Q^T W r_b  (W = bm1)                                             :305-308
+                 c_b = D^{-1} c (back substitution, linear_system)                   :387-403
+                 rot = mod(rot, bst_snp) + 1;  Y(:,rot) = r_b                         :310-311
+                 r_b += X c_b;  X(:,rot) = r_b                                        :313-318
+
+The fields are the velocities only (``opcopy`` / ``opsub2`` act on vx, vy, [vz]), so the
+accelerator runs in its own velocity-only context (weights ``bm1``).  Dots, updates and the
+combination are the library's device kernels; the k x k triangular solve is on the host.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .layout import NekLayout
+from .vector import NekContext, NekVector
+
+
+def velocity_layout(lay: NekLayout) -> NekLayout:
+    return NekLayout(lay.ldim, lay.lx1, lay.lx2, lay.nelgv, n_scalars=0, ifpo=False, rank=lay.rank, world=lay.world)
+
+
+def linear_system(m: np.ndarray, inp: np.ndarray) -> np.ndarray:
+    """Back substitution with the upper triangle of m (fixedp.f90:387-403)."""
+    n = inp.shape[0]
+    out = np.zeros(n)
+    for j in range(n - 1, -1, -1):
+        v = inp[j]
+        for k in range(j + 1, n):
+            v = v - m[j, k] * out[k]
+        out[j] = v / m[j, j]
+    return out
+
+
+class BoostConv:
+    def __init__(self, ctx: NekContext, bst_snp: int = 10):
+        if ctx.layout.n_scalars or ctx.layout.n_p:
+            raise ValueError("BoostConv works on a velocity-only context (velocity_layout)")
+        self.ctx, self.n = ctx, bst_snp
+        self.X, self.Y, self.Q = ctx.basis(bst_snp), ctx.basis(bst_snp), ctx.basis(bst_snp)
+        self.dd = np.ones((bst_snp, bst_snp))
+        self.rot = 0  # 0-based rot
+        self.init = False
+        self._dum = ctx.vector()
+        self._r = torch.zeros(1, dtype=torch.float64, device=ctx.device)
+
+    def _dot(self, a: NekVector, b: NekVector) -> float:
+        return self.ctx.dot(a, b, time=False)
+
+    def qr_dec(self) -> None:
+        """Single-pass MGS QR of Y into Q and dd, reference operation order (fixedp.f90:331-385)."""
+        ctx, n = self.ctx, self.n
+        dd = np.zeros((n, n))
+        dum = self._dum
+        for j in range(n):
+            dum.copy_from(self.Y[j], time=False)
+            for i in range(j):
+                r = self._dot(dum, self.Q[i])
+                dd[i, j] = r
+                dum.axpby(1.0, self.Q[i], -r)
+            norma = self._dot(dum, dum)
+            if j == 0:
+                norma = float(np.sqrt(norma))
+                dum.scal(1.0 / norma)
+                self.Q[0].copy_from(dum, time=False)
+                dd[0, 0] = norma
+                continue
+            if norma < 1e-60:
+                norma = 1.0
+                self.Q[j].zero()
+            else:
+                dum.scal(1.0 / np.sqrt(norma))
+                self.Q[j].copy_from(dum, time=False)
+            dd[j, j] = np.sqrt(norma)
+        self.dd = dd
+
+    def core(self, rb: NekVector) -> None:
+        """boostconv_core(rbx, rby, rbz): rb is corrected in place."""
+        if not self.init:
+            for B in (self.X, self.Y, self.Q):
+                for i in range(self.n):
+                    B[i].zero()
+            self.Y[0].copy_from(rb, time=False)
+            self.X[0].copy_from(rb, time=False)
+            self.dd = np.ones((self.n, self.n))
+            self.rot = 0
+            self.init = True
+            return
+        r = self.rot
+        self.Y[r].axpby(1.0, rb, -1.0)           # y_rot -= rb
+        self.X[r].axpby(1.0, self.Y[r], -1.0)    # x_rot -= y_rot
+        self.qr_dec()
+        cc = np.array([self._dot(rb, self.Q[j]) for j in range(self.n)])
+        ccb = linear_system(self.dd, cc)
+        self.rot = (r + 1) % self.n
+        self.Y[self.rot].copy_from(rb, time=False)
+        h = torch.as_tensor(-ccb).to(self.ctx.device)  # rb <- rb - X(-ccb) = rb + X ccb
+        self.ctx.call("nkv_block_update", self.ctx.w.data_ptr(), self.X.ptr, self.n, h.data_ptr(), rb.ptr, None,
+                      self.ctx.ws.data_ptr(), 0, self.ctx.stream)
+        self.X[self.rot].copy_from(rb, time=False)

@@ -352,3 +352,50 @@ def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):
     i = (gamma * aIm[:n] + delta * aRe[:n]) / den
     aRe[:n], aIm[:n] = r, i
     return dRe, dIm, aRe, aIm
+
+
+def boostconv_core(state, rb, w, nv_total):
+    """fixedp.f90:267-329 in numpy on velocity-only vectors (reference order).  ``state`` is a dict
+    created empty by the caller; rb (length nv_total) is corrected in place."""
+    n = state.setdefault("n", 10)
+    dot = lambda a, b: float(np.sum(a * np.tile(w, a.size // w.size) * b))  # noqa: E731
+    if not state.get("init"):
+        state.update(X=np.zeros((n, rb.size)), Y=np.zeros((n, rb.size)), Q=np.zeros((n, rb.size)),
+                     dd=np.ones((n, n)), rot=0, init=True)
+        state["Y"][0] = rb
+        state["X"][0] = rb
+        return
+    X, Y, Q = state["X"], state["Y"], state["Q"]
+    r = state["rot"]
+    Y[r] = Y[r] - rb
+    X[r] = X[r] - Y[r]
+    dd = np.zeros((n, n))
+    Q[:] = 0.0
+    dum = Y[0].copy()
+    norma = np.sqrt(dot(dum, dum))
+    Q[0] = dum * (1.0 / norma)
+    dd[0, 0] = norma
+    for j in range(1, n):
+        dum = Y[j].copy()
+        for i in range(j):
+            dd[i, j] = dot(dum, Q[i])
+            dum = dum - Q[i] * dd[i, j]
+        norma = dot(dum, dum)
+        if norma < 1e-60:
+            norma = 1.0
+            Q[j] = 0.0
+        else:
+            Q[j] = dum * (1.0 / np.sqrt(norma))
+        dd[j, j] = np.sqrt(norma)
+    cc = np.array([dot(rb, Q[j]) for j in range(n)])
+    ccb = np.zeros(n)
+    for j in range(n - 1, -1, -1):
+        v = cc[j]
+        for k in range(j + 1, n):
+            v = v - dd[j, k] * ccb[k]
+        ccb[j] = v / dd[j, j]
+    state["rot"] = (r + 1) % n
+    Y[state["rot"]] = rb
+    for j in range(n):
+        rb += X[j] * ccb[j]
+    X[state["rot"]] = rb
