@@ -108,3 +108,30 @@ def test_gmres_resolvent_composite(gpu):
     got = x.to_packed()
     live = [f * LAY.sv + i for f in range(LAY.n_wf) for i in range(LAY.n_v)]
     np.testing.assert_allclose(got[live], bx[live] / (1.0 - d[live]), rtol=1e-9, atol=1e-12)
+
+
+def test_drivers_linear_stability_and_transient_growth(gpu, tmp_path):
+    from nekstab_next_amd import fld
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.drivers import linear_stability_analysis, transient_growth_analysis
+
+    ctx, w, d, vh, A = _setup()
+    M, W, idx = _dense(ctx, A, w)
+    lam = np.linalg.eigvals(M)
+    lam = lam[np.argsort(-np.abs(lam))]
+    seed = ctx.vector()
+    seed.fill_hash(5)
+    t = 2.5
+    out = linear_stability_analysis(ctx, A, seed, t, KrylovSchurConfig(k_dim=30, schur_tgt=3, maxmodes=2),
+                                    outdir=str(tmp_path), session="box")
+    np.testing.assert_allclose(out["eigvals"][:3], lam[:3], rtol=1e-10)
+    np.testing.assert_allclose(out["eigvals_ns"][:3], np.log(lam[:3].astype(complex)) / t, rtol=1e-10)
+    spec = np.loadtxt(tmp_path / "Spectrum_NSd.dat")
+    np.testing.assert_allclose(spec[0, 0], np.log(abs(lam[0])) / t, rtol=1e-6)
+    f = fld.read_fld(str(tmp_path / "dRebox0.f00001"))
+    assert f.rdcode == "U" and f.nelgt == LAY.nelgv
+    g = transient_growth_analysis(ctx, A, seed, k_dim=40, nev=2, tolerance=1e-8, outdir=str(tmp_path),
+                                  session="box")
+    s_exact = np.linalg.svd(np.sqrt(W)[:, None] * M / np.sqrt(W)[None, :], compute_uv=False)
+    np.testing.assert_allclose(g["gain"][:2], s_exact[:2] ** 2, rtol=1e-10)
+    assert (tmp_path / "pUbox0.f00001").exists() and (tmp_path / "Spectrum_Sp.dat").exists()
