@@ -151,3 +151,39 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         update_hessenberg_matrix(ctx, Q, mstep, f, Hd, mode)
         if on_step is not None:
             on_step(mstep)
+
+
+class FactorizationGraph:
+    """HIP-graph replay of ``arnoldi_factorization(mstart..mend)``.
+
+    Every launch of a factorisation (matvec kernels, the Gram–Schmidt kernels, the RCCL all-reduces
+    when the process group is ``nccl``) is captured once per (mstart, mend, transpose) into a
+    ``torch.cuda.CUDAGraph`` on the compute stream and replayed: no host work and no launch
+    latency between kernels.  All buffers (basis, H, f, workspace, partial vectors) are allocated
+    before capture and never move.  The operator must be capturable (device kernels only: no host
+    synchronisation in ``matvec``); a ``gloo`` group (host all-reduce) cannot be captured, so
+    ``usable()`` is False for it and callers fall back to eager launches."""
+
+    def __init__(self, ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, f: NekVector,
+                 mode: str = "cgs2"):
+        self.ctx, self.op, self.Q, self.Hd, self.f, self.mode = ctx, op, Q, Hd, f, mode
+        self.graphs = {}
+
+    def usable(self) -> bool:
+        return self.ctx.comm.world == 1 or self.ctx.comm.backend == "nccl"
+
+    def run(self, mstart: int, mend: int, transpose: bool = False) -> None:
+        if mend < mstart:
+            return
+        key = (mstart, mend, transpose)
+        g = self.graphs.get(key)
+        if g is None:
+            timer, self.ctx.timer = self.ctx.timer, None
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.ctx.device)
+            with torch.cuda.graph(g):
+                arnoldi_factorization(self.ctx, self.op, self.Q, self.Hd, mstart, mend, f=self.f, mode=self.mode,
+                                      transpose=transpose)
+            self.ctx.timer = timer
+            self.graphs[key] = g
+        g.replay()

@@ -15,6 +15,7 @@ class KrylovSchurConfig:
     seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "as_is"
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
+    graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)
 
 
 @dataclass

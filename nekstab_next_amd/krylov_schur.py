@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import lapack
-from .arnoldi import HessenbergDev, arnoldi_factorization
+from .arnoldi import FactorizationGraph, HessenbergDev, arnoldi_factorization
 from .config import KrylovSchurConfig
 from .operators import LinearOperator
 from .vector import Basis, NekContext, NekVector
@@ -117,8 +117,14 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     schur_cnt = 0
     res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
     hook = None if on_step is None else (lambda mstep: on_step(mstep, Q, Hd))
+    graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode) if (cfg.graphs and hook is None) else None
+    if graphs is not None and not graphs.usable():
+        graphs = None
     while True:
-        arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook)
+        if graphs is not None:
+            graphs.run(mstart, k, transpose)
+        else:
+            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook)
         H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
         ctx.check_nan()
         vals, vecs = lapack.eig(H[:k, :k])

@@ -205,3 +205,27 @@ def test_config5_direct_adjoint_biorthogonal(gpu):
     o = orc.biorthogonalize(L, w, *(syn.to_reference_order(lay, x.to_packed()) for x in (dRe, dIm, aRe, aIm)))
     for x, y in zip((dRe, dIm, aRe, aIm), o):
         np.testing.assert_allclose(syn.to_reference_order(lay, x.to_packed()), y, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("opname", ["diag", "rot2"])
+def test_graph_replay_is_bit_identical(gpu, opname):
+    """cfg.graphs=True replays captured factorisations: same kernels in the same order, so the
+    Krylov–Schur result equals the eager run bit for bit (restarts exercise several mstart graphs)."""
+    lay = cylinder_layout(400)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=40)
+    if opname == "diag":
+        d, _ = syn.diag_spectrum(lay)
+        op = DiagOperator(ctx, d)
+        cfg = dict(k_dim=16, schur_tgt=5)
+    else:
+        c, s, dr, _ = syn.rot2_operator(lay)
+        op = Rot2Operator(ctx, c, s, dr)
+        cfg = dict(k_dim=24, schur_tgt=2)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    r1 = krylov_schur(ctx, op, seed, KrylovSchurConfig(**cfg))
+    r2 = krylov_schur(ctx, op, seed, KrylovSchurConfig(graphs=True, **cfg))
+    assert r1.schur_cnt == r2.schur_cnt and r1.schur_cnt >= 1
+    np.testing.assert_array_equal(r1.vals, r2.vals)
+    np.testing.assert_array_equal(r1.H, r2.H)
