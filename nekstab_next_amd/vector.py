@@ -56,7 +56,8 @@ class NekContext:
         self.timer = None  # optional profiling.PhaseTimer (per-phase HIP events)
         self.lib = _lib.load()
         f64 = dict(dtype=torch.float64, device=self.device)
-        self.w = torch.zeros(layout.sv, **f64)
+        # at least one tile: an empty shard (rank with no elements) still passes a valid pointer
+        self.w = torch.zeros(max(layout.sv, 4096), **f64)
         if weights is None:
             self.w[: layout.n_v] = 1.0
         else:

@@ -301,3 +301,66 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
     t = lay.time_offset
     href = Qh @ (wfull * fref) + Qh[:, t] * fref[t]
     np.testing.assert_allclose(hout.cpu().numpy(), href, rtol=1e-12, atol=1e-12 * np.abs(href).max())
+
+
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2"])
+def test_arnoldi_with_time_component_vs_oracle(gpu, mode):
+    """uparam(1)==2.1: the scalar `time` enters k_dot (krylov_subspace.f90:52-54) and follows every
+    update; the operator propagates it (time_scale)."""
+    lay = LAYOUTS["3d_scalar"]
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=True)
+    L = olayout(lay, time_in_dot=True)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d, time_scale=0.7)
+    m = 12
+    Q = ctx.basis(m + 1)
+    q0 = syn.hash_vector(lay, 5)
+    q0[lay.time_offset] = 0.3
+    Q[0].from_packed(q0)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, m)
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode=mode)
+    H = Hd.download()
+    Qr = np.zeros((m + 1, L.len))
+    Qr[0] = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, Qr[0])
+    Hr = np.zeros((m + 1, m))
+    dref = syn.to_reference_order(lay, d)
+    orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
+    assert np.max(np.abs(H - Hr)) <= 1e-12 * np.max(np.abs(Hr))
+    times = Q.storage.cpu().numpy()[:, lay.time_offset]
+    np.testing.assert_allclose(times, Qr[:, -1], rtol=1e-10, atol=1e-14)
+    assert np.any(np.abs(times) > 1e-3)  # the time component is really carried
+
+
+def test_empty_shard(gpu):
+    """A rank that owns no elements (more ranks than elements): every entry point is a no-op on
+    its data and contributes zero partials; only the replicated time term is counted (rank 0)."""
+    class Solo:
+        rank, world, backend = 0, 3, None
+
+        def allreduce_(self, t):
+            return t
+
+    g = NekLayout(ldim=2, lx1=4, lx2=2, nelgv=2)
+    lay = g.shard(0, 3)  # elements [0*2//3, 1*2//3) = [0, 0)
+    assert lay.nelv == 0 and lay.n_v == 0 and lay.sv == 0
+    ctx = NekContext(lay, weights=np.zeros(0), comm=Solo(), max_cols=8)
+    Q = ctx.basis(5)
+    for i in range(5):
+        Q[i].fill_hash(i)
+    f = ctx.vector()
+    f.fill_hash(9)
+    h = ctx.h1[:4]
+    ctx.call("nkv_block_dot", ctx.w.data_ptr(), Q.ptr, 4, f.ptr, h.data_ptr(), ctx.ws.data_ptr(), 0, ctx.stream)
+    assert not np.any(h.cpu().numpy())
+    from nekstab_next_amd._lib import NKV_TIME_DOT
+    ctx.call("nkv_block_update_dot", ctx.w.data_ptr(), Q.ptr, 4, h.data_ptr(), f.ptr, ctx.h2[:4].data_ptr(),
+             ctx.ws.data_ptr(), NKV_TIME | NKV_TIME_DOT, ctx.stream)
+    ctx.call("nkv_block_update", ctx.w.data_ptr(), Q.ptr, 4, h.data_ptr(), f.ptr, ctx.scal[4:5].data_ptr(),
+             ctx.ws.data_ptr(), NKV_NORM2, ctx.stream)
+    assert ctx.scal[4].item() == 0.0 and not np.any(ctx.h2[:4].cpu().numpy())
+    V = torch.eye(4, dtype=torch.float64, device=ctx.device).flatten()
+    ctx.call("nkv_rotate", Q.ptr, 4, V.data_ptr(), 4, ctx.stream)
+    torch.cuda.synchronize()
