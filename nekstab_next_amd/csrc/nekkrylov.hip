@@ -45,6 +45,9 @@ namespace {
 #ifndef NKV_FUSE_G
 #define NKV_FUSE_G 1024  // workgroups of the fused update+dot
 #endif
+#ifndef NKV_FUSE_PF
+#define NKV_FUSE_PF 0  // 1: prefetch the next tile's columns across the per-tile barrier
+#endif
 
 constexpr int kThreads = 256;                       // 4 waves of 64
 static_assert(NKV_TILE % (kThreads * NKV_PAIRS * 2) == 0, "kernel tile must divide the padding");
@@ -135,6 +138,11 @@ __device__ __forceinline__ double block_sum(double v, double* lds4) {
 }
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+// uniform base + 32-bit byte offset: lets the compiler use the SGPR-base/VGPR-offset load form
+// instead of a 64-bit VGPR address per column (fewer VGPRs in the register-resident kernels)
+__device__ __forceinline__ const double* at_b(const double* base, uint32_t byte_off) {
+    return reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + byte_off);
+}
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 // Loads of streamed basis columns: each byte is read once per pass and, at the sizes that matter,
@@ -361,22 +369,43 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 #pragma unroll
     for (int i = 0; i < CPW; ++i) acc[i] = 0.0;
     int buf = 0;
+    auto load_tile = [&](double2 (&q)[CPW], int64_t t) {
+        const uint32_t rb = ((uint32_t)(t * kFuseRows) + 2u * lane) * 8u;  // rows < 2^29 (checked)
+#pragma unroll
+        for (int i = 0; i < CPW - 1; ++i) q[i] = ldq(at_b(qcol[i], rb));
+        // CPW = ceil(j/NW): only the last slot can lie past j (wave-uniform test, never fetched)
+        q[CPW - 1] = (wv + NW * (CPW - 1) < j) ? ldq(at_b(qcol[CPW - 1], rb)) : make_double2(0.0, 0.0);
+    };
+    double2 q[CPW];
+#if NKV_FUSE_PF
+    double2 qn[CPW];
+    if ((int64_t)blockIdx.x < tiles_total) load_tile(q, blockIdx.x);
+#endif
     for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x, buf ^= 1) {
         const uint32_t r = (uint32_t)(t * kFuseRows) + 2u * lane;
-        double2 q[CPW];
-#pragma unroll
-        for (int i = 0; i < CPW - 1; ++i) q[i] = ldq(qcol[i] + r);
-        // CPW = ceil(j/NW): only the last slot can lie past j (wave-uniform test, never fetched)
-        q[CPW - 1] = (wv + NW * (CPW - 1) < j) ? ldq(qcol[CPW - 1] + r) : make_double2(0.0, 0.0);
+#if !NKV_FUSE_PF
+        load_tile(q, t);
+#endif
         double2 s = make_double2(0.0, 0.0);
 #pragma unroll
         for (int i = 0; i < CPW; ++i) {
             s.x = fma(hc[i], q[i].x, s.x);
             s.y = fma(hc[i], q[i].y, s.y);
         }
-        const double2 fv = ld2(f + r);
+        const double2 fv = ld2(at_b(f, r * 8u));
+        const bool weighted = t < tiles_w;
+        // weights are loaded before any prefetch: vmcnt retires in order, so a load issued after
+        // the prefetch would wait for it
+        const double2 ww = weighted ? ld2(at_b(w, (r - (uint32_t)((t / tiles_per_field) * sv)) * 8u)) : make_double2(0.0, 0.0);
         part[buf][wv][lane] = s;
+#if NKV_FUSE_PF
+        const int64_t tn = t + gridDim.x;
+        if (tn < tiles_total) load_tile(qn, tn);  // stays in flight across the barrier below
+        // LDS-only wait + raw barrier: a __syncthreads() would also drain vmcnt (the prefetch)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
         __syncthreads();
+#endif
         double2 tot = part[buf][0][lane];
 #pragma unroll
         for (int k = 1; k < NW; ++k) {
@@ -385,14 +414,16 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
             tot.y += p.y;
         }
         const double2 f1 = make_double2(fv.x - tot.x, fv.y - tot.y);
-        if (wv == 0) st2(f + r, f1);
-        if (t < tiles_w) {
-            const uint32_t wr = r - (uint32_t)((t / tiles_per_field) * sv);
-            const double2 ww = ld2(w + wr);
+        if (wv == 0) st2(const_cast<double*>(at_b(f, r * 8u)), f1);
+        if (weighted) {
             const double a = ww.x * f1.x, b = ww.y * f1.y;
 #pragma unroll
             for (int i = 0; i < CPW; ++i) acc[i] = fma(q[i].y, b, fma(q[i].x, a, acc[i]));
         }
+#if NKV_FUSE_PF
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) q[i] = qn[i];
+#endif
         // no second barrier: the next tile writes the other buffer, and a wave can only reach the
         // barrier after it once every wave has passed this tile's barrier (and read this buffer)
     }
@@ -876,7 +907,7 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
     const unsigned upd_flags = (flags & NKV_TIME) ? NKV_TIME : 0u;
     const unsigned dot_flags = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
-    if (j > 256 || rows_of(L) >= (int64_t)1 << 32) {  // tile does not fit registers: two passes
+    if (j > 256 || rows_of(L) >= (int64_t)1 << 29) {  // tile does not fit registers / 32-bit offsets
         CHECK(nkv_block_update(L, w, Q, j, h_dev, f, nullptr, ws, upd_flags, stream));
         return launch_block_dot(L, w, Q, L->ld, j, f, hout_dev, ws, dot_flags, S(stream));
     }

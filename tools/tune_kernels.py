@@ -35,6 +35,11 @@ VARIANTS = {
     "nt_fg512": {"NKV_NT": 1, "NKV_FUSE_G": 512},
     "nt_fg2048": {"NKV_NT": 1, "NKV_FUSE_G": 2048},
     "nt_f16_g512": {"NKV_NT": 1, "NKV_FUSE_NW": 16, "NKV_FUSE_G": 512},
+    "pf": {"NKV_FUSE_PF": 1},
+    "pf_g512": {"NKV_FUSE_PF": 1, "NKV_FUSE_G": 512},
+    "pf_g256": {"NKV_FUSE_PF": 1, "NKV_FUSE_G": 256},
+    "pf_nw16": {"NKV_FUSE_PF": 1, "NKV_FUSE_NW": 16},
+    "pf_nw16_g256": {"NKV_FUSE_PF": 1, "NKV_FUSE_NW": 16, "NKV_FUSE_G": 256},
 }
 
 
