@@ -135,7 +135,7 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
 
 /* ---- Krylov–Schur restart (a10, schur_condensation eigensolvers.f90:421-442) --------------
  * In place: Q[:,0:k] <- Q[:,0:k] * V, V k-by-k column-major (leading dim ldv) in device memory.
- * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 256. */
+ * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 576. */
 int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream);
 
 /* ---- synthetic operators (the matvec boundary, linear_operators.f90:17-23) ----------------

@@ -55,8 +55,7 @@ static_assert(NKV_TILE % (kThreads * NKV_PAIRS_SMALL * 2) == 0, "kernel tile mus
 constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots per column
 constexpr int kColUnroll = NKV_COLU;                 // columns in flight per thread (block dot)
 constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
-constexpr int kRotRows = 64;                         // rows per rotation tile
-constexpr int kRotMaxK = 256;
+constexpr int kRotMaxK = 576;                        // rotation: 64-row tiles up to k=256, 32-row beyond
 
 thread_local char g_err[512] = "";
 
@@ -522,45 +521,50 @@ __global__ __launch_bounds__(kThreads) void k_blas1(double* x, const double* y, 
 }
 
 // ------------------------------------------------------------------------------------------
-// Restart rotation, in place:  Q[:, 0:k] <- Q[:, 0:k] V.   One workgroup owns 64 rows: the
-// 64 x k input tile is staged in LDS (so outputs can overwrite those rows), V streams through
-// LDS in 16 x 64 chunks, each thread accumulates a 4 x 4 register block.
+// Restart rotation, in place:  Q[:, 0:k] <- Q[:, 0:k] V.   One workgroup owns R rows: the
+// R x k input tile is staged in LDS (so outputs can overwrite those rows), V streams through LDS
+// in 16 x CC chunks, each thread accumulates a 4 x 4 register block.  R = 64 up to k = 256,
+// R = 32 up to k = 576 (the tile must fit the 160 KiB LDS).
 // ------------------------------------------------------------------------------------------
+template <int R>
 __global__ __launch_bounds__(kThreads) void k_rotate(double* __restrict__ Q, int64_t ld, int k,
                                                      const double* __restrict__ V, int ldv,
                                                      int64_t n_tiles) {
+    constexpr int RG = R / 4;          // row groups of 4
+    constexpr int CG = kThreads / RG;  // column groups of 4
+    constexpr int CC = 4 * CG;         // columns per chunk
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* A = sm;                 // [k][kRotRows]
-    double* Vs = sm + k * kRotRows;  // [16][64]
-    const int tr = threadIdx.x & 15;  // rows 4*tr .. 4*tr+3
-    const int tc = threadIdx.x >> 4;  // cols 4*tc .. 4*tc+3 of the current 64-column chunk
+    double* A = sm;            // [k][R]
+    double* Vs = sm + k * R;   // [16][CC]
+    const int tr = threadIdx.x % RG;  // rows 4*tr .. 4*tr+3
+    const int tc = threadIdx.x / RG;  // cols 4*tc .. 4*tc+3 of the current chunk
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const int64_t row0 = tile * kRotRows;
+        const int64_t row0 = tile * R;
         __syncthreads();
-        for (int idx = threadIdx.x; idx < k * (kRotRows / 2); idx += kThreads) {
-            const int c = idx / (kRotRows / 2), r2 = idx % (kRotRows / 2);
-            st2(A + c * kRotRows + 2 * r2, ld2(Q + (int64_t)c * ld + row0 + 2 * r2));
+        for (int idx = threadIdx.x; idx < k * (R / 2); idx += kThreads) {
+            const int c = idx / (R / 2), r2 = idx % (R / 2);
+            st2(A + c * R + 2 * r2, ld2(Q + (int64_t)c * ld + row0 + 2 * r2));
         }
         __syncthreads();
-        for (int cc = 0; cc < k; cc += 64) {
+        for (int cc = 0; cc < k; cc += CC) {
             double acc[4][4];
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
             for (int ii = 0; ii < k; ii += 16) {
-                for (int e = threadIdx.x; e < 16 * 64; e += kThreads) {
-                    const int i = e >> 6, c = e & 63;
+                for (int e = threadIdx.x; e < 16 * CC; e += kThreads) {
+                    const int i = e / CC, c = e % CC;
                     const int gi = ii + i, gc = cc + c;
                     Vs[e] = (gi < k && gc < k) ? V[gi + (int64_t)gc * ldv] : 0.0;
                 }
                 __syncthreads();
                 const int imax = min(16, k - ii);
                 for (int i = 0; i < imax; ++i) {
-                    const double2 a01 = ld2(A + (ii + i) * kRotRows + 4 * tr);
-                    const double2 a23 = ld2(A + (ii + i) * kRotRows + 4 * tr + 2);
-                    const double2 v01 = ld2(Vs + i * 64 + 4 * tc);
-                    const double2 v23 = ld2(Vs + i * 64 + 4 * tc + 2);
+                    const double2 a01 = ld2(A + (ii + i) * R + 4 * tr);
+                    const double2 a23 = ld2(A + (ii + i) * R + 4 * tr + 2);
+                    const double2 v01 = ld2(Vs + i * CC + 4 * tc);
+                    const double2 v23 = ld2(Vs + i * CC + 4 * tc + 2);
                     const double av[4] = {a01.x, a01.y, a23.x, a23.y};
                     const double vv[4] = {v01.x, v01.y, v23.x, v23.y};
 #pragma unroll
@@ -989,18 +993,24 @@ int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int l
     if (!V_dev) return fail(NKV_EINVAL, "V_dev is NULL");
     if (k < 1 || k > kRotMaxK) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d]", k, kRotMaxK);
     if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
-    const size_t lds = ((size_t)k * kRotRows + 16 * 64) * sizeof(double);
     static bool attr_set = false;
     if (!attr_set) {
-        NKV_HIP(hipFuncSetAttribute((const void*)k_rotate, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(((size_t)kRotMaxK * kRotRows + 16 * 64) * sizeof(double))));
+        NKV_HIP(hipFuncSetAttribute((const void*)k_rotate<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)((256 * 64 + 16 * 64) * sizeof(double))));
+        NKV_HIP(hipFuncSetAttribute((const void*)k_rotate<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)((kRotMaxK * 32 + 16 * 128) * sizeof(double))));
         attr_set = true;
     }
-    const int64_t n_tiles = rows_of(L) / kRotRows;
+    const bool big = k > 256;
+    const int R = big ? 32 : 64;
+    const size_t lds = ((size_t)k * R + 16 * (big ? 128 : 64)) * sizeof(double);
+    const int64_t n_tiles = rows_of(L) / R;
     int64_t g = n_tiles < 4096 ? n_tiles : 4096;
     if (g < 1) return NKV_OK;
-    hipLaunchKernelGGL(k_rotate, dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k, V_dev,
-                       ldv, n_tiles);
+    if (big)
+        hipLaunchKernelGGL(k_rotate<32>, dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k, V_dev, ldv, n_tiles);
+    else
+        hipLaunchKernelGGL(k_rotate<64>, dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k, V_dev, ldv, n_tiles);
     NKV_LAUNCHED();
     return NKV_OK;
 }

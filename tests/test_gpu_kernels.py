@@ -177,7 +177,7 @@ def test_k_matmul_vs_oracle(gpu):
     np.testing.assert_allclose(syn.to_reference_order(lay, out.to_packed()), ref, rtol=1e-13, atol=1e-14)
 
 
-@pytest.mark.parametrize("k", [1, 7, 16, 64, 100, 129, 256])
+@pytest.mark.parametrize("k", [1, 7, 16, 64, 100, 129, 256, 257, 300, 576])
 def test_rotate_vs_oracle(gpu, k):
     lay = LAYOUTS["2d"]
     ctx, _ = make_ctx(lay)
@@ -193,7 +193,11 @@ def test_rotate_vs_oracle(gpu, k):
     Vd = torch.as_tensor(V.ravel(order="F").copy()).to(ctx.device)
     ctx.call("nkv_rotate", Q.ptr, k, Vd.data_ptr(), k, ctx.stream)
     Qk = np.ascontiguousarray(Qref[:k])
-    orc.lib().orc_rotate(ctypes.byref(L.c), Qk, k, np.ascontiguousarray(V.ravel(order="F")))
+    orc.set_threads(8 if k > 128 else 1)
+    try:
+        orc.lib().orc_rotate(ctypes.byref(L.c), Qk, k, np.ascontiguousarray(V.ravel(order="F")))
+    finally:
+        orc.set_threads(1)
     got = Q.storage.cpu().numpy()
     for i in range(k):
         np.testing.assert_allclose(syn.to_reference_order(lay, got[i]), Qk[i], rtol=1e-12, atol=1e-13)
@@ -270,7 +274,7 @@ def test_shape_errors(gpu):
         ctx.call("nkv_block_dot", ctx.w.data_ptr(), v.ptr, 0, v.ptr, ctx.h1.data_ptr(), ctx.ws.data_ptr(), 0,
                  ctx.stream)
     with pytest.raises(NkvError):
-        ctx.call("nkv_rotate", v.ptr, 300, ctx.h1.data_ptr(), 300, ctx.stream)
+        ctx.call("nkv_rotate", v.ptr, 600, ctx.h1.data_ptr(), 600, ctx.stream)
 
 
 @pytest.mark.parametrize("j", [1, 5, 8, 9, 31, 64, 65, 128, 129, 200, 256, 300])
