@@ -138,6 +138,13 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
  * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 576. */
 int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream);
 
+/* Partial restart rotation, in place: Q[:,0:n_out] <- Q[:,0:k] * V[:,0:n_out], 1 <= n_out <= k.
+ * Columns n_out..k-1 are left as they were.  schur_condensation only keeps the mstart selected
+ * Schur vectors (eigensolvers.f90:416-459: Q(mstart+1..k) are overwritten by the next
+ * factorisation before being read), so the restart calls this with n_out = mstart. */
+int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out,
+                    void* stream);
+
 /* ---- synthetic operators (the matvec boundary, linear_operators.f90:17-23) ----------------
  * op_diag: y = d .* x over every stored row; y.time = time_scale * x.time.
  * op_rot2: per weighted point i, (u,v) = (wf_0[i], wf_1[i]):

@@ -89,6 +89,19 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // this offset.
 inline int64_t rows_of(const nkv_layout* L) { return (int64_t)L->n_wf * L->sv + L->sp; }
 
+// Compute units of the current device (cached per device id; 256 on MI355X).
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        cus[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                       ? n : 256;
+    }
+    return cus[dev];
+}
+
 int check_layout(const nkv_layout* L) {
     if (!L) return fail(NKV_EINVAL, "layout is NULL");
     if (L->n_wf < 1 || L->n_v < 0 || L->n_p < 0)
@@ -588,6 +601,148 @@ __global__ __launch_bounds__(kThreads) void k_rotate(double* __restrict__ Q, int
 }
 
 // ------------------------------------------------------------------------------------------
+// Restart rotation on the f64 matrix cores:  Q[:, 0:n_out] <- Q[:, 0:k] V[:, 0:n_out].
+// Computed as the transpose, D = V^T Q^T, so that D's fast (lane & 15) index runs along the
+// points: every 16-lane group stores 128 contiguous bytes of one column.  One workgroup owns R
+// rows; its R x k input tile is staged in LDS before any output is written (in place is safe).
+// Waves: WR = R/16 row blocks x WC = 4/WR column groups; each wave keeps MB 16x16 accumulators
+// (v_mfma_f64_16x16x4_f64: A[l&15][l>>4], B[l>>4][l&15], D[(l>>4)+4r][l&15]).  V streams through
+// LDS KB rows at a time, stored column-major with an odd stride (KB + 1); the Q tile is
+// XOR-swizzled (column ^ 16 on odd rows): both ds_read_b64 operand reads are conflict-free.
+// ------------------------------------------------------------------------------------------
+typedef double nkv_f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int rot_swz(int row, int col) { return col ^ ((row & 1) << 4); }
+
+template <int R, int CC, int KB>
+__global__ __launch_bounds__(kThreads) void k_rotate_mfma(double* __restrict__ Q, int64_t ld, int k,
+                                                          const double* __restrict__ V, int ldv, int n_out,
+                                                          int64_t n_tiles) {
+    constexpr int WR = R / 16, WC = 4 / WR, MB = CC / 16 / WC;
+    static_assert(WR * WC == 4 && MB >= 1, "tile shape");
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int kpad = (k + 3) & ~3;
+    double* A = sm;                 // [kpad][R]
+    double* Vs = sm + kpad * R;     // [CC][KB + 1]: odd stride, conflict-free column reads
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave % WR, wc = wave / WR;
+    const int lr = lane & 15, lk = lane >> 4;
+    for (int idx = k * R + threadIdx.x; idx < kpad * R; idx += kThreads) A[idx] = 0.0;  // k..kpad rows
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t row0 = tile * R;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < k * (R / 2); idx += kThreads) {
+            const int c = idx / (R / 2), r = 2 * (idx % (R / 2));
+            st2(A + c * R + rot_swz(c, r), ld2(Q + (int64_t)c * ld + row0 + r));
+        }
+        for (int cc = 0; cc < n_out; cc += CC) {
+            nkv_f64x4 acc[MB];
+#pragma unroll
+            for (int m = 0; m < MB; ++m) acc[m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
+            const int nact = (min(CC, n_out - cc) + 15) / 16;   // active 16-column blocks in the chunk
+            for (int ii = 0; ii < k; ii += KB) {
+                __syncthreads();
+                for (int e = threadIdx.x; e < KB * CC; e += kThreads) {
+                    const int i = e % KB, c = e / KB;   // i fastest: coalesced reads of column-major V
+                    const int gi = ii + i, gc = cc + c;
+                    Vs[c * (KB + 1) + i] = (gi < k && gc < n_out) ? V[gi + (int64_t)gc * ldv] : 0.0;
+                }
+                __syncthreads();
+                const int kmax = min(KB, kpad - ii);
+                for (int kk = 0; kk < kmax; kk += 4) {
+                    const int ia = ii + kk + lk, iv = kk + lk;
+                    const double b = A[ia * R + rot_swz(ia, wr * 16 + lr)];
+#pragma unroll
+                    for (int m = 0; m < MB; ++m) {
+                        const int blk = wc + WC * m;
+                        if (blk < nact) {
+                            const double a = Vs[(blk * 16 + lr) * (KB + 1) + iv];
+                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[m], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                const int blk = wc + WC * m;
+                if (blk < nact) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int gc = cc + blk * 16 + lk + 4 * r;
+                        if (gc < n_out) Q[(int64_t)gc * ld + row0 + wr * 16 + lr] = acc[m][r];
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Restart rotation, streaming form (n_out <= 16*MB and V[:, 0:n_out] fits LDS): V is staged in
+// LDS once per workgroup; afterwards every wave streams its own NB x 16-row slabs of Q straight
+// from HBM into the MFMA B operand, with no barrier and no LDS round trip for Q.  All k inputs
+// of a slab are consumed before any of its n_out outputs is stored, and no other wave touches
+// those rows, so in place is safe.  A workgroup's waves cover one contiguous WAVES*NB*16-row
+// tile, so each column is read in WAVES*NB*128-byte runs.  LDS: Vs[c * kp + i], kp = 2 (mod 32)
+// doubles: the two 16-lane k-rows of a ds_read_b64 land on disjoint bank pairs.
+// ------------------------------------------------------------------------------------------
+template <int NB, int MB, int WAVES, int U>
+__global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict__ Q, int64_t ld, int k,
+                                                              const double* __restrict__ V, int ldv, int n_out,
+                                                              int kp, int64_t n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double Vs[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+    // Vs[c][i] for c < 16*MB, i < kp (zero beyond n_out / k: the last 4U-step batch needs no guard)
+    for (int e = threadIdx.x; e < MB * 16 * kp; e += WAVES * 64) {
+        const int c = e / kp, i = e % kp;
+        Vs[e] = (i < k && c < n_out) ? V[i + (int64_t)c * ldv] : 0.0;
+    }
+    __syncthreads();
+    const double* vs = Vs + lr * kp + lk;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t row0 = (tile * WAVES + wave) * (NB * 16);
+        const double* q = Q + row0 + lr;
+        nkv_f64x4 acc[NB][MB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int m = 0; m < MB; ++m) acc[nb][m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
+        for (int i0 = 0; i0 < k; i0 += 4 * U) {
+            double b[U][NB];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + 4 * u + lk;
+                const double* qi = q + (int64_t)(i < k ? i : 0) * ld;
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) b[u][nb] = i < k ? qi[nb * 16] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m) {
+                    const double a = vs[m * 16 * kp + i0 + 4 * u];
+#pragma unroll
+                    for (int nb = 0; nb < NB; ++nb)
+                        acc[nb][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u][nb], acc[nb][m], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gc = m * 16 + lk + 4 * r;
+                if (gc < n_out) {
+#pragma unroll
+                    for (int nb = 0; nb < NB; ++nb) Q[(int64_t)gc * ld + row0 + nb * 16 + lr] = acc[nb][m][r];
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // synthetic operators and data
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__ d,
@@ -987,12 +1142,35 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
     return NKV_OK;
 }
 
-int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream) {
-    CHECK(check_layout(L));
-    CHECK(check_ptr(Q, "Q"));
-    if (!V_dev) return fail(NKV_EINVAL, "V_dev is NULL");
-    if (k < 1 || k > kRotMaxK) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d]", k, kRotMaxK);
-    if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
+#ifndef NKV_ROT_VALU
+#define NKV_ROT_VALU 0   // 1: the VALU (4x4 register block) rotation instead of the f64 MFMA one
+#endif
+#ifndef NKV_ROT_SMALLR
+#define NKV_ROT_SMALLR 64   // MFMA rotation tile rows for k <= 256 (64 or 32)
+#endif
+
+extern "C++" template <int R, int CC, int KB>
+static int launch_rotate_mfma(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
+                              void* stream) {
+    const int kpad = (k + 3) & ~3;
+    const size_t lds = ((size_t)kpad * R + (size_t)(KB + 1) * CC) * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NKV_HIP(hipFuncSetAttribute((const void*)k_rotate_mfma<R, CC, KB>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    if (lds > 160 * 1024) return fail(NKV_EINVAL, "rotate: k=%d needs %zu B of LDS", k, lds);
+    const int64_t n_tiles = rows_of(L) / R;
+    const int64_t g = n_tiles < 4096 ? n_tiles : 4096;
+    if (g < 1) return NKV_OK;
+    hipLaunchKernelGGL((k_rotate_mfma<R, CC, KB>), dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k,
+                       V, ldv, n_out, n_tiles);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+static int rotate_valu(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream) {
     static bool attr_set = false;
     if (!attr_set) {
         NKV_HIP(hipFuncSetAttribute((const void*)k_rotate<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1013,6 +1191,81 @@ int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int l
         hipLaunchKernelGGL(k_rotate<64>, dim3((unsigned)g), dim3(kThreads), lds, S(stream), Q, L->ld, k, V_dev, ldv, n_tiles);
     NKV_LAUNCHED();
     return NKV_OK;
+}
+
+#ifndef NKV_ROT_STREAM
+#define NKV_ROT_STREAM 1   // 0: never use the streaming rotation
+#endif
+#ifndef NKV_ROT_WAVES
+#define NKV_ROT_WAVES 16
+#endif
+#ifndef NKV_ROT_NB
+#define NKV_ROT_NB 1
+#endif
+#ifndef NKV_ROT_U
+#define NKV_ROT_U 8   // k-steps of 4 loaded per batch
+#endif
+
+extern "C++" template <int MB>
+static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
+                                int kp, size_t lds, void* stream) {
+    // register budget: ~21*MB + 55 VGPRs (U = 8); 16 waves/WG allow 128 per lane, so wide column blocks
+    // run with half the waves (256 VGPRs)
+    constexpr int NB = NKV_ROT_NB, W = MB <= 3 ? NKV_ROT_WAVES : NKV_ROT_WAVES / 2, U = NKV_ROT_U;
+    auto kern = k_rotate_stream<NB, MB, W, U>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NKV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    const int64_t rows_tile = (int64_t)W * NB * 16;
+    const int64_t n_tiles = rows_of(L) / rows_tile;
+    if (n_tiles < 1) return NKV_OK;
+    int per_cu = (int)((160 * 1024) / lds);
+    per_cu = per_cu < 1 ? 1 : (per_cu > 32 / W ? 32 / W : per_cu);   // LDS and 32 waves per CU
+    const int64_t g0 = (int64_t)device_cus() * per_cu;
+    const int64_t g = n_tiles < g0 ? n_tiles : g0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, kp,
+                       n_tiles);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    if (!V_dev) return fail(NKV_EINVAL, "V_dev is NULL");
+    if (k < 1 || k > kRotMaxK) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d]", k, kRotMaxK);
+    if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
+    if (n_out < 1 || n_out > k) return fail(NKV_EINVAL, "rotate: n_out=%d outside [1, k=%d]", n_out, k);
+    if (NKV_ROT_VALU && n_out == k) return rotate_valu(L, Q, k, V_dev, ldv, stream);
+    if (NKV_ROT_STREAM && rows_of(L) % ((int64_t)NKV_ROT_WAVES * NKV_ROT_NB * 16) == 0) {
+        const int kp = ((k + 31) & ~31) + 2;
+        const int nact = (n_out + 15) / 16;
+        const size_t lds = (size_t)nact * 16 * kp * sizeof(double);
+        if (lds <= 160 * 1024) {
+            switch (nact) {
+                case 1: return launch_rotate_stream<1>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 2: return launch_rotate_stream<2>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 3: return launch_rotate_stream<3>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 4: return launch_rotate_stream<4>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 5: return launch_rotate_stream<5>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 6: return launch_rotate_stream<6>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 7: return launch_rotate_stream<7>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                case 8: return launch_rotate_stream<8>(L, Q, k, V_dev, ldv, n_out, kp, lds, stream);
+                default: break;
+            }
+        }
+    }
+    if (k <= 256) {
+        if (NKV_ROT_SMALLR == 32) return launch_rotate_mfma<32, 128, 16>(L, Q, k, V_dev, ldv, n_out, stream);
+        return launch_rotate_mfma<64, 128, 16>(L, Q, k, V_dev, ldv, n_out, stream);
+    }
+    return launch_rotate_mfma<32, 128, 8>(L, Q, k, V_dev, ldv, n_out, stream);
+}
+
+int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream) {
+    return nkv_rotate_cols(L, Q, k, V_dev, ldv, k, stream);
 }
 
 int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y, double time_scale,

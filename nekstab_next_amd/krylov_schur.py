@@ -12,7 +12,8 @@ Control flow restated one-for-one:
 
 ``schur_condensation``: b = H(k+1,k) e_k; (T, Z) = dgees(H_k) sorted |lambda|>0.9; select
 (|lambda| >= 1-schur_del) U (nev+4 largest); dtrsen; zero the unwanted blocks; Q(:,1:k) <- Q(:,1:k) Z
-(device, in place — the reference copies the whole basis twice, :421-432); H(ms+1,:) = b^T Z;
+(device, in place, only the ms kept columns — the reference copies the whole basis twice and
+rotates all k, :421-442); H(ms+1,:) = b^T Z;
 mstart = ms+1; Q(mstart) <- Q(k+1).
 
 The dense k x k work runs on the host (lapack.py), identically on every rank.
@@ -63,8 +64,12 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
     H[:k, :k] = T
     H[:ms, ms:k] = 0.0
     H[ms:k + 1, :] = 0.0
-    Zd = torch.as_tensor(np.asfortranarray(Z).ravel(order="F")).to(ctx.device)
-    ctx.call("nkv_rotate", Q.ptr, int(k), Zd.data_ptr(), int(k), ctx.stream)
+    if ms > 0:
+        # Only Q(1:ms) survive the restart: Q(ms+1) <- Q(k+1) below and Q(ms+2..k) are rewritten by
+        # the next factorisation before any read, so the device rotation writes ms columns
+        # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.
+        Zd = torch.as_tensor(np.asfortranarray(Z[:, :ms]).ravel(order="F")).to(ctx.device)
+        ctx.call("nkv_rotate_cols", Q.ptr, int(k), Zd.data_ptr(), int(k), int(ms), ctx.stream)
     H[ms, :] = b_vec @ Z
     mstart = ms + 1
     # Q(mstart) <- Q(k+1): nopcopy moves the fields only, not time (:458-459)

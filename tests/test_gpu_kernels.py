@@ -205,6 +205,34 @@ def test_rotate_vs_oracle(gpu, k):
     np.testing.assert_array_equal(syn.to_reference_order(lay, got[k]), Qref[k])  # column k untouched
 
 
+@pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 20), (129, 17), (256, 255), (300, 150), (576, 33)])
+def test_rotate_cols_vs_oracle(gpu, k, n_out):
+    """Partial restart rotation: Q[:, :n_out] = Q[:, :k] V[:, :n_out]; columns n_out..k untouched."""
+    lay = LAYOUTS["2d"]
+    ctx, _ = make_ctx(lay)
+    L = olayout(lay)
+    Q = ctx.basis(k + 1)
+    Qref = np.zeros((k + 1, L.len))
+    for i in range(k + 1):
+        v = syn.hash_vector(lay, 11 + i)
+        Q[i].from_packed(v)
+        Qref[i] = syn.to_reference_order(lay, v)
+    V = np.linalg.qr(np.random.default_rng(k + n_out).standard_normal((k, k)))[0]
+    Vd = torch.as_tensor(np.asfortranarray(V[:, :n_out]).ravel(order="F")).to(ctx.device)
+    ctx.call("nkv_rotate_cols", Q.ptr, k, Vd.data_ptr(), k, n_out, ctx.stream)
+    Qk = Qref[:k].copy()
+    orc.set_threads(8 if k > 128 else 1)
+    try:
+        orc.lib().orc_rotate(ctypes.byref(L.c), Qk, k, np.ascontiguousarray(V.ravel(order="F")))
+    finally:
+        orc.set_threads(1)
+    got = Q.storage.cpu().numpy()
+    for i in range(n_out):
+        np.testing.assert_allclose(syn.to_reference_order(lay, got[i]), Qk[i], rtol=1e-12, atol=1e-13)
+    for i in range(n_out, k + 1):
+        np.testing.assert_array_equal(syn.to_reference_order(lay, got[i]), Qref[i])
+
+
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
@@ -275,6 +303,9 @@ def test_shape_errors(gpu):
                  ctx.stream)
     with pytest.raises(NkvError):
         ctx.call("nkv_rotate", v.ptr, 600, ctx.h1.data_ptr(), 600, ctx.stream)
+    for n_out in (0, 5):   # n_out outside [1, k]
+        with pytest.raises(NkvError):
+            ctx.call("nkv_rotate_cols", v.ptr, 4, ctx.h1.data_ptr(), 4, n_out, ctx.stream)
 
 
 @pytest.mark.parametrize("j", [1, 5, 8, 9, 31, 64, 65, 128, 129, 200, 256, 300])

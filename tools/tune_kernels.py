@@ -40,6 +40,13 @@ VARIANTS = {
     "pf_g256": {"NKV_FUSE_PF": 1, "NKV_FUSE_G": 256},
     "pf_nw16": {"NKV_FUSE_PF": 1, "NKV_FUSE_NW": 16},
     "pf_nw16_g256": {"NKV_FUSE_PF": 1, "NKV_FUSE_NW": 16, "NKV_FUSE_G": 256},
+    "rot_valu": {"NKV_ROT_VALU": 1},
+    "rot_r32": {"NKV_ROT_SMALLR": 32},
+    "rot_staged": {"NKV_ROT_STREAM": 0},
+    "rot_w8": {"NKV_ROT_WAVES": 8},
+    "rot_w8_nb2": {"NKV_ROT_WAVES": 8, "NKV_ROT_NB": 2},
+    "rot_u2": {"NKV_ROT_U": 2},
+    "rot_u8": {"NKV_ROT_U": 8},
 }
 
 
@@ -57,7 +64,7 @@ def build(names):
         assert p.wait() == 0
 
 
-def run(names, E, rounds, js):
+def run(names, E, rounds, js, only=None):
     import numpy as np
     import torch
 
@@ -91,6 +98,7 @@ def run(names, E, rounds, js):
     h2 = torch.zeros(jmax + 1, dtype=torch.float64, device=dev)
     nrm = torch.zeros(8, dtype=torch.float64, device=dev)
     N, Nw, nv = lay.N, lay.N_w, lay.n_v
+    V = torch.eye(jmax, dtype=torch.float64, device=dev).flatten()  # rotation by I keeps Q bounded
 
     def ops(L, j):
         return {
@@ -100,6 +108,9 @@ def run(names, E, rounds, js):
                             8.0 * (j * N + 2 * N + nv)),
             "update_dot": (lambda: L.nkv_block_update_dot(Lp, w.data_ptr(), Q.data_ptr(), j, h.data_ptr(), f.data_ptr(), h2.data_ptr(), ws.data_ptr(), 0x1, st),
                            8.0 * (j * N + 2 * N + nv)),
+            "rotate": (lambda: L.nkv_rotate(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, st), 16.0 * j * N),
+            "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
+                            8.0 * (j + max(1, j // 6)) * N),
         }
 
     res = {}
@@ -107,6 +118,8 @@ def run(names, E, rounds, js):
         for n in names:
             for j in js:
                 for opname, (fn, nbytes) in ops(libs[n], j).items():
+                    if only and opname not in only:
+                        continue
                     fn()  # warm
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
@@ -121,7 +134,11 @@ def run(names, E, rounds, js):
     out = {}
     for (n, j, op), v in sorted(res.items()):
         out[f"{n} j={j} {op}"] = dict(median_gbs=float(np.median(v)), min_gbs=float(np.min(v)), max_gbs=float(np.max(v)))
-        print(f"{n:10s} j={j:4d} {op:12s} median {np.median(v):8.1f} GB/s  (min {np.min(v):.1f})", flush=True)
+        extra = ""
+        if op == "rotate":  # 2 N k^2 flop over 16 N k bytes
+            tf = np.median(v) * 1e9 / (16.0 * j * N) * 2.0 * N * j * j / 1e12
+            extra = f"  = {tf:.1f} TFLOP/s fp64"
+        print(f"{n:10s} j={j:4d} {op:12s} median {np.median(v):8.1f} GB/s  (min {np.min(v):.1f}){extra}", flush=True)
     return out
 
 
@@ -132,12 +149,14 @@ if __name__ == "__main__":
     ap.add_argument("--E", type=int, default=44176)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--js", default="32,128")
+    ap.add_argument("--ops", default="", help="comma list (default: all)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tune.json"))
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.cmd == "build":
         build(names)
     else:
-        out = run(names, a.E, a.rounds, [int(x) for x in a.js.split(",")])
+        out = run(names, a.E, a.rounds, [int(x) for x in a.js.split(",")],
+                  [x for x in a.ops.split(",") if x])
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
         json.dump(out, open(a.out, "w"), indent=1)
