@@ -18,7 +18,9 @@ step, so it moves fewer bytes than SURVEY.md §8(d)'s 4-pass model
 that model divided by the same time is reported separately as ``effective_gbs_survey_model`` (the
 work definition the CPU baseline is also measured in).  ``roofline`` is the dominant kernel family
 (block multi-dot, fused update+dot, or update+norm) timed live with HIP events on the launch
-stream.
+stream.  ``restart`` (outside the timed region) times one Krylov–Schur condensation of the final
+factorisation: the kept-column rotation the solver runs (HBM-bound) and the reference's full
+k-column rotation (2Nk^2 flop, priced against the fp64 peak; f64 MFMA).
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 spec (vector = matrix on CDNA4); SURVEY.md §8(d) ridge ~10 flop/B
 
 
 def survey_model_bytes(N, N_w, n_v, m):
@@ -119,6 +122,7 @@ def main():
     ap.add_argument("--cpu-E", type=int, default=512)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-restart", action="store_true", help="skip the restart-rotation measurement")
     args = ap.parse_args()
 
     import torch
@@ -127,7 +131,8 @@ def main():
     from nekstab_next_amd import synthetic as syn
     from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
     from nekstab_next_amd.comm import init_from_env
-    from nekstab_next_amd.krylov_schur import prepare_seed
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.krylov_schur import prepare_seed, schur_condensation
     from nekstab_next_amd.layout import box3d_layout
     from nekstab_next_amd.operators import DiagOperator
     from nekstab_next_amd.profiling import PhaseTimer
@@ -179,6 +184,40 @@ def main():
     ctx.timer = None
     phases = timer.summary()
     ctx.check_nan()
+
+    # Krylov–Schur restart on the final factorisation (outside the timed region; reported beside
+    # the metric): the kept-column rotation the solver runs, and the reference's
+    # full k-column rotation priced against the fp64 matrix peak.
+    restart = None
+    if not args.no_restart:
+        rt = PhaseTimer(dev)
+        ctx.timer = rt
+        # the shift-invert spectrum is not inside the unit disc (every |mu| >= 1 - schur_del would be
+        # kept); scale H by its spectral radius as a time-stepper's exp(L dt) spectrum would be —
+        # same Schur vectors, the selection rule then keeps the leading cluster + nev + 4
+        H = Hd.download()
+        H /= np.max(np.abs(vals))
+        t1 = time.perf_counter()
+        mstart, _sel = schur_condensation(ctx, H, Q, m, KrylovSchurConfig(k_dim=m, schur_tgt=4))
+        torch.cuda.synchronize(dev)
+        cond_ms = (time.perf_counter() - t1) * 1e3
+        V = torch.as_tensor(np.linalg.qr(np.random.default_rng(5).standard_normal((m, m)))[0].ravel(order="F")
+                            .copy()).to(dev)
+        for _ in range(2):
+            rt.begin("rotate_full")
+            ctx.call("nkv_rotate", Q.ptr, m, V.data_ptr(), m, ctx.stream)
+            rt.end("rotate_full", 16.0 * lay.N * m)
+        ctx.timer = None
+        rp = rt.summary()
+        kept, full = rp["rotate"], rp["rotate_full"]
+        full_tf = 2.0 * lay.N * m * m / (full["avg_ms"] * 1e-3) / 1e12
+        restart = {
+            "mstart": int(mstart), "condensation_wall_ms": round(cond_ms, 2),
+            "rotate_kept_ms": round(kept["avg_ms"], 3), "rotate_kept_gbs": round(kept["gbps"], 1),
+            "rotate_kept_frac_hbm": round(kept["gbps"] / HBM_PEAK_GBS, 4),
+            "rotate_full_ms": round(full["avg_ms"], 3), "rotate_full_tflops": round(full_tf, 2),
+            "rotate_full_frac_fp64": round(full_tf / FP64_PEAK_TFLOPS, 4),
+        }
 
     ms_per_step = elapsed / args.steps * 1e3
     nv_g = glay.pts_v * glay.nelgv
@@ -248,6 +287,7 @@ def main():
             "ritz_top8_rel_err": top_err,
             "ritz_converged": int(conv.sum()),
             "cpu_baseline": ({k: v for k, v in cpu.items() if k != "seconds"} if cpu else None),
+            "restart": restart,
         }
         print(json.dumps(out), flush=True)
 

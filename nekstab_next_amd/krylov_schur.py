@@ -69,7 +69,11 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
         # the next factorisation before any read, so the device rotation writes ms columns
         # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.
         Zd = torch.as_tensor(np.asfortranarray(Z[:, :ms]).ravel(order="F")).to(ctx.device)
+        if ctx.timer:
+            ctx.timer.begin("rotate")
         ctx.call("nkv_rotate_cols", Q.ptr, int(k), Zd.data_ptr(), int(k), int(ms), ctx.stream)
+        if ctx.timer:
+            ctx.timer.end("rotate", 8.0 * ctx.layout.N * (k + ms))
     H[ms, :] = b_vec @ Z
     mstart = ms + 1
     # Q(mstart) <- Q(k+1): nopcopy moves the fields only, not time (:458-459)

@@ -27,6 +27,16 @@ def main():
         print(f"{fam:14s} {calls:13d} {tot / calls / 1e6:15.4f} {ev}")
     print("(rocprof counts every launch incl. warm-up and the j=1 seed dots; events cover the timed steps; "
           "event brackets include the ~5 us second-stage reduction kernel)")
+    rs = bench.get("restart")
+    if rs:
+        # restart rotations: k_rotate_stream<NB, MB, W, U>, MB = ceil(n_out / 16) column blocks
+        mb_kept = (rs["mstart"] - 1 + 15) // 16
+        for label, mb, ms in (("rotate kept", mb_kept, rs["rotate_kept_ms"]), ("rotate full", 8, rs["rotate_full_ms"])):
+            rows = [r for r in stats if f"k_rotate_stream<1, {mb}," in r["Name"]]
+            if rows:
+                calls = sum(int(r["Calls"]) for r in rows)
+                avg = sum(float(r["TotalDurationNs"]) for r in rows) / calls / 1e6
+                print(f"{label:14s} {calls:13d} {avg:15.4f} {'':>16s} {ms:14.4f} {ms / avg:7.3f}")
 
 
 if __name__ == "__main__":

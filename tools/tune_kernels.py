@@ -76,6 +76,8 @@ def run(names, E, rounds, js, only=None):
     for n in names:
         L = ctypes.CDLL(os.path.join(VDIR, f"lib_{n}.so"))
         for name, (res, args) in _lib._SIGNATURES.items():
+            if not hasattr(L, name):   # an older build compared against this one
+                continue
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
         libs[n] = L
@@ -119,6 +121,8 @@ def run(names, E, rounds, js, only=None):
             for j in js:
                 for opname, (fn, nbytes) in ops(libs[n], j).items():
                     if only and opname not in only:
+                        continue
+                    if opname == "rotate_part" and not hasattr(libs[n], "nkv_rotate_cols"):
                         continue
                     fn()  # warm
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
