@@ -22,6 +22,10 @@ FAMILIES = {
     "finish": ("k_finish",),
     "op_diag": ("k_op_diag",),
     "copy": ("k_blas1<1>",),
+    # restart rotations of bench.py's restart leg (8 B/lane loads: the x2 FETCH correction is for
+    # 16 B/lane reads, so these rows show how far the correction holds for narrower loads)
+    "rotate_kept": ("k_rotate_stream<1, 1,",),
+    "rotate_full": ("k_rotate_stream<1, 8,",),
 }
 
 
