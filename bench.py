@@ -67,10 +67,21 @@ def executed_bytes(N, N_w, n_v, m, mode):
     return tot
 
 
-def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float, variant: str = "mgs2"):
     """The reference algorithm (MGS + full re-orthogonalisation with per-field weighted dots, copy
     -> dot -> cmult -> sub2, krylov_decomposition.f90:155-180) restated in C (oracle/), on the same
-    operator family at a bounded sample size, timed on this host.  Steps run until ``budget_s``."""
+    operator family at a bounded sample size, timed on this host.  Steps run until ``budget_s``.
+    ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
 
@@ -84,9 +95,13 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
     d, _ = syn.laplacian_shift_invert(lay)
     dref = syn.to_reference_order(lay, d)
     orc.set_threads(threads)
+    if variant == "cgs2":
+        orc.cgs2_lib().cpu_cgs2_set_threads(threads)
+        step = orc.cgs2_lib().cpu_cgs2_update_hessenberg
+    else:
+        step = orc.lib().orc_update_hessenberg
     Q = np.zeros((m + 1, L.len))
     Q[0] = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 11)))
-    H = np.zeros((m + 1, m))
     f = L.zeros()
     wrk = L.zeros()
     c = ctypes.byref(L.c)
@@ -94,7 +109,7 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
     for j in range(1, m + 1):
         orc.lib().orc_op_diag(c, dref, Q[j - 1], f, 0.0)
         col = np.zeros(j + 1)
-        orc.lib().orc_update_hessenberg(c, w, col, f, Q[:j], j, wrk)  # Q rows are contiguous views
+        step(c, w, col, f, Q[:j], j, wrk)  # Q rows are contiguous views
         Q[j] = f
         done_bytes += 8.0 * (2 * j * (lay.N_w + lay.N) + 2 * (lay.N_w + lay.n_v) + 4 * lay.N + lay.n_v + 2 * lay.N)
         done_bytes += 8.0 * 3 * lay.N
@@ -103,11 +118,12 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float):
             break
     dt = time.perf_counter() - t0
     orc.set_threads(1)
+    what = ("reference MGS2 Arnoldi (C restatement, oracle/nekstab_oracle.c)" if variant == "mgs2" else
+            "optimised CPU: blocked OpenMP CGS2 (oracle/cpu_cgs2.c, AVX2/FMA)")
     return dict(value=done_bytes / dt / 1e9, unit="GB/s", cores=threads, kind="port",
-                sample=(f"reference MGS2 Arnoldi (C restatement, oracle/nekstab_oracle.c) on the same 3-D "
-                        f"lx1=8 layout at E={E_sample} (N={lay.N}), steps j=1..{steps} of m={m}, "
-                        f"{dt:.1f} s, {threads} OpenMP threads; GB/s in SURVEY.md §8(d)'s CGS2 byte model "
-                        f"(compare with effective_gbs_survey_model)"),
+                sample=(f"{what} on the same 3-D lx1=8 layout at E={E_sample} (N={lay.N}), steps j=1..{steps} "
+                        f"of m={m}, {dt:.1f} s, {threads} thread(s) on {cpu_model()}; GB/s in SURVEY.md "
+                        f"§8(d)'s CGS2 byte model (compare with effective_gbs_survey_model)"),
                 seconds=dt)
 
 
@@ -246,10 +262,12 @@ def main():
             traffic = None
 
     if rank == 0:
-        cpu = None
+        cpu = cpu1 = cpu_opt = None
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)
+            threads = min(16, os.cpu_count() or 1)   # the box's CPU share is 16 cores
             cpu = cpu_baseline(args.cpu_E, m, threads, args.cpu_budget)
+            cpu1 = cpu_baseline(args.cpu_E, m, 1, args.cpu_budget / 2)
+            cpu_opt = cpu_baseline(args.cpu_E, m, threads, args.cpu_budget / 2, variant="cgs2")
         out = {
             "metric": "Arnoldi-step GB/s (achieved HBM) + Ritz-value rel-err, N=1e8 m=128",
             "value": round(value, 2),
@@ -287,6 +305,8 @@ def main():
             "ritz_top8_rel_err": top_err,
             "ritz_converged": int(conv.sum()),
             "cpu_baseline": ({k: v for k, v in cpu.items() if k != "seconds"} if cpu else None),
+            "cpu_baseline_1core": ({k: v for k, v in cpu1.items() if k != "seconds"} if cpu1 else None),
+            "cpu_optimised": ({k: v for k, v in cpu_opt.items() if k != "seconds"} if cpu_opt else None),
             "restart": restart,
         }
         print(json.dumps(out), flush=True)

@@ -87,6 +87,26 @@ def set_threads(n: int) -> None:
     lib().orc_set_threads(int(n))
 
 
+_cgs2 = None
+
+
+def cgs2_lib():
+    """The timed "optimised CPU" line (oracle/cpu_cgs2.c: blocked OpenMP CGS2) — bench.py only."""
+    global _cgs2
+    if _cgs2 is None:
+        path = os.path.join(_HERE, "libcpucgs2.so")
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        L = ctypes.CDLL(path)
+        L.cpu_cgs2_set_threads.restype, L.cpu_cgs2_set_threads.argtypes = None, [c_int]
+        L.cpu_cgs2_update_hessenberg.restype = None
+        L.cpu_cgs2_update_hessenberg.argtypes = [_LP, _D, _D, _D, _D, c_int, _D]
+        _cgs2 = L
+    return _cgs2
+
+
 class OLayout:
     """Unpadded reference layout [vx | vy | (vz) | t.. | pr | time] of one shard."""
 
