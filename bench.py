@@ -8,16 +8,19 @@ MI355X GPUs with RCCL all-reduce" — 3-D spectral-element layout lx1=8, lx2=6, 
 element-contiguous shard; dots are all-reduced (RCCL) once per Gram–Schmidt pass.
 
 One *step* = one full m-step Arnoldi factorisation from the normalised seed (prepare_seed, then
-m x [synthetic matvec + CGS2 Gram–Schmidt + normalise]) followed by the host Ritz extraction
-(H download, dgeev, residuals) — the work of one Krylov–Schur cycle before any restart.
+m x [synthetic matvec + block Gram–Schmidt + normalise], the closing re-orthogonalisation)
+followed by the host Ritz extraction (H download, dgeev, residuals) — the work of one
+Krylov–Schur cycle before any restart.
 
 ``value`` = achieved HBM GB/s of the whole step: the bytes the executed algorithm moves (global N,
-all ranks; see ``executed_bytes``) / step time.  The fused CGS2 reads the basis 3x per Arnoldi
-step, so it moves fewer bytes than SURVEY.md §8(d)'s 4-pass model
+all ranks; see ``executed_bytes``) / step time.  The default ``--mode dcgs2`` (CGS2 with delayed
+re-orthogonalisation) reads the basis 2x per Arnoldi step (``cgs2``: 3x), so it moves fewer bytes
+than SURVEY.md §8(d)'s 4-pass model
   B(j) = 8 [2j(N_w+N) + 2(N_w+n_v) + 4N + n_v + 2N]  (+ 8*3N matvec);
 that model divided by the same time is reported separately as ``effective_gbs_survey_model`` (the
-work definition the CPU baseline is also measured in).  ``roofline`` is the dominant kernel family
-(block multi-dot, fused update+dot, or update+norm) timed live with HIP events on the launch
+work definition the CPU baseline is also measured in; it exceeds the HBM peak because the
+executed algorithm does half the model's reads).  ``roofline`` is the dominant kernel family
+(two-vector multi-dot, dual update, or the cgs2 kernels) timed live with HIP events on the launch
 stream.  ``restart`` (outside the timed region) times one Krylov–Schur condensation of the final
 factorisation: the kept-column rotation the solver runs (HBM-bound) and the reference's full
 k-column rotation (2Nk^2 flop, priced against the fp64 peak; f64 MFMA).
@@ -61,9 +64,13 @@ def executed_bytes(N, N_w, n_v, m, mode):
             tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
         elif mode == "cgs2-unfused":
             tot += 2 * dot + upd + (upd + 8.0 * n_v)
+        elif mode == "dcgs2":   # two-vector dot over j columns; dual update over j-1 columns
+            tot += 8.0 * (j * N_w + 2 * N_w + n_v) + 8.0 * ((j - 1) * N + 4 * N + n_v)
         else:
             raise ValueError(mode)
         tot += 8.0 * 2 * N + 8.0 * 3 * N
+    if mode == "dcgs2":  # closing re-orthogonalisation of q_{m+1}: dot, update, normalise
+        tot += 8.0 * ((m + 1) * N_w + N_w + n_v) + 8.0 * (m * N + 2 * N) + 8.0 * 2 * N
     return tot
 
 
@@ -134,7 +141,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--E", type=int, default=44176, help="global elements (44,176 -> N=1.0e8)")
     ap.add_argument("--m", type=int, default=128)
-    ap.add_argument("--mode", default="cgs2")
+    ap.add_argument("--mode", default="dcgs2", help="dcgs2 (default) | cgs2 | cgs2-unfused")
     ap.add_argument("--cpu-E", type=int, default=512)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -248,7 +255,8 @@ def main():
     top_err = float(np.max(np.abs(vals[:8] - exact[:8]) / np.abs(exact[:8])))
 
     # dominant kernel family (rank-local launches; bytes are this rank's shard)
-    dom = max(("block_dot", "update_dot", "block_update"), key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
+    dom = max(("block_dot", "update_dot", "block_update", "block_dot2", "dcgs2_update"),
+              key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
     ph = phases[dom]
     achieved = ph["gbps"]
     traffic = None
@@ -283,7 +291,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (diagonalised shift-invert Laplacian, hashed seed, GLL x J_e weights)",
             "config": {
-                "workload": "config3: m-step Arnoldi (CGS2) + Ritz extraction, shift-invert Laplacian",
+                "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
                 "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
                 "m": m, "mode": args.mode, "parallelism": f"element-shard x{world} + RCCL allreduce",
             },

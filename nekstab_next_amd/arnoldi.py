@@ -16,6 +16,14 @@ Two orthogonalisation modes share the rest of the path:
   the device.  ~3jN streamed doubles per step instead of the reference's ~20jN, and 3
   collectives instead of (2k+2)*n_fields.  ``"cgs2-unfused"`` runs the middle pass as two kernels
   (4 reads of Q), kept for A/B measurement.
+* ``"dcgs2"``: classical Gram–Schmidt with DELAYED re-orthogonalisation (low-synchronisation
+  CGS2, cf. Świrydowicz et al. 2020, Bielich et al. 2022): step j projects A q_j once against the
+  basis while re-orthogonalising the still-provisional q_j in the same pass — one two-vector
+  multi-dot over Q (+ one all-reduce of 2j), a small device kernel that corrects the previous H
+  column and derives the coefficients, one update pass over Q that finalises q_j and projects
+  f (+ the ||f||^2 all-reduce).  Two reads of Q per step instead of three; the last vector of a
+  factorisation is re-orthogonalised once at the end, so on return Q and H are exactly an
+  Arnoldi factorisation, as with cgs2.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
 
@@ -132,19 +140,85 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         ctx.timer.end("finish", 16.0 * ctx.layout.N)
 
 
+def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector) -> None:
+    """Step j (1-based) of DCGS2 Arnoldi: Q[0:j-1] final, Q[j-1] provisional, f = A Q[j-1].
+    On return Q[j-1] is final, Q[j] provisional, H columns 0..j-2 final and column j-1 provisional."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    m = j - 1
+    h, coef, nrm = ctx.hd[: 2 * j], ctx.coef, ctx.scal[3:4]
+    qj = Q.col_ptr(m)
+    if tm:
+        tm.begin("block_dot2")
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, qj, f.ptr, h.data_ptr(), ws, tf, st)
+    if tm:
+        tm.end("block_dot2", 8.0 * (j * lay.N_w + 2 * lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), h[j:].data_ptr(), Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws,
+                st)
+    if tm:
+        tm.begin("dcgs2_update")
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, h.data_ptr(), coef.data_ptr(), qj, f.ptr, nrm.data_ptr(), ws,
+             NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
+    if tm:
+        tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N + lay.n_v))
+    ctx.comm.allreduce_(nrm)
+    if tm:
+        tm.begin("finish")
+    ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), Q.col_ptr(j), j, coef[m:].data_ptr(), None,
+             Hd.col_ptr(m), 0, st)
+    if tm:
+        tm.end("finish", 16.0 * lay.N)
+
+
+def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
+    """Re-orthogonalise the provisional Q[m] against Q[0:m] and correct H row m (end of a DCGS2
+    factorisation of m steps)."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    h, coef = ctx.hd[: m + 1], ctx.coef
+    qm = Q.col_ptr(m)
+    if tm:
+        tm.begin("block_dot")
+    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, qm, h.data_ptr(), ws, tf, st)
+    if tm:
+        tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws, st)
+    if tm:
+        tm.begin("block_update")
+    ctx.call("nkv_block_update", w, Q.ptr, m, h.data_ptr(), qm, None, ws, NKV_TIME, st)
+    if tm:
+        tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
+    ctx.call("nkv_normalize_dev", qm, coef[2 * m + 3:].data_ptr(), None, 0, st)
+
+
 def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,
                           mend: int, f: NekVector | None = None, mode: str = "cgs2", transpose: bool = False,
                           on_step=None) -> None:
     """k-step Arnoldi from column ``mstart`` to ``mend`` (1-based, inclusive), as
     krylov_decomposition.f90:68-96: f = A q_mstep; orthonormalise; Q(mstep+1) = f.
 
-    ``on_step(mstep)`` is called after each step (hook for checkpointing, cf. ifres at :84)."""
+    ``on_step(mstep)`` is called after each step (hook for checkpointing, cf. ifres at :84); it
+    needs the finished column after every step, so with a hook ``"dcgs2"`` runs as ``"cgs2"``."""
     if mend < mstart:
         return
     if Q.k < mend + 1:
         raise ValueError("basis too small")
     if f is None:
         f = ctx.vector()
+    if mode == "dcgs2" and on_step is None:
+        if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+            raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        for mstep in range(mstart, mend + 1):
+            (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
+            _dcgs2_step(ctx, Q, Hd, mstep, f)
+        _dcgs2_close(ctx, Q, Hd, mend)
+        return
+    if mode == "dcgs2":
+        mode = "cgs2"
     for mstep in range(mstart, mend + 1):
         x = Q[mstep - 1]
         (op.rmatvec if transpose else op.matvec)(x, f)

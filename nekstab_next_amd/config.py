@@ -11,7 +11,8 @@ class KrylovSchurConfig:
     eigen_tol: float = 1e-6   # Ritz residual tolerance (:11)
     schur_del: float = 0.1    # keep |lambda| >= 1 - schur_del at restarts (:12)
     maxmodes: int = 20        # max eigenmodes exported (:13)
-    mode: str = "cgs2"        # "cgs2" (block, MI355X hot path) | "mgs2" (reference operation order)
+    mode: str = "dcgs2"       # "dcgs2" (block CGS2, delayed re-orth.: 2 reads of Q per step, the MI355X
+    #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order)
     seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "as_is"
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it

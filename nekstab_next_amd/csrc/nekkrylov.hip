@@ -448,6 +448,247 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
+// DCGS2 (classical Gram–Schmidt with delayed re-orthogonalisation) — two reads of Q per step.
+//
+// Two-vector multi-dot: partials[c][b] = q_c . (w x), partials[j + c][b] = q_c . (w y) in ONE
+// read of Q (x = the provisional q_j, y = A q_j).  Same grid and tiling as k_block_dot.
+// ------------------------------------------------------------------------------------------
+template <int kPairs>
+__global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restrict__ Q, int64_t ld,
+                                                         int j, const double* __restrict__ x,
+                                                         const double* __restrict__ y,
+                                                         const double* __restrict__ w, int64_t sv,
+                                                         int tiles_per_field,
+                                                         double* __restrict__ partials, int B) {
+    constexpr int kTile = kThreads * kPairs * 2;
+    constexpr int U = 2;  // columns in flight (two right-hand sides double the registers per column)
+    extern __shared__ double red[];  // [4 waves][2j]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
+    __syncthreads();
+    const int64_t fb = (int64_t)blockIdx.y * sv;
+    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 wx[kPairs], wy[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 wv = ld2(w + r0 + k * 2 * kThreads);
+            const double2 xv = ld2(x + fb + r0 + k * 2 * kThreads);
+            const double2 yv = ld2(y + fb + r0 + k * 2 * kThreads);
+            wx[k] = make_double2(wv.x * xv.x, wv.y * xv.y);
+            wy[k] = make_double2(wv.x * yv.x, wv.y * yv.y);
+        }
+        const double* qb = Q + fb + r0;
+        for (int c = 0; c < j; c += U) {
+            double2 q[U][kPairs];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k)
+                    q[u][k] = (c + u < j) ? ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads) : make_double2(0.0, 0.0);
+            double s[2 * U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double a = 0.0, b = 0.0;
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    a = fma(q[u][k].x, wx[k].x, a);
+                    a = fma(q[u][k].y, wx[k].y, a);
+                    b = fma(q[u][k].x, wy[k].x, b);
+                    b = fma(q[u][k].y, wy[k].y, b);
+                }
+                s[u] = a;
+                s[U + u] = b;
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+                for (int u = 0; u < 2 * U; ++u) s[u] += __shfl_xor(s[u], off, 64);
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (c + u < j) {
+                        red[wave * 2 * j + c + u] += s[u];
+                        red[wave * 2 * j + j + c + u] += s[U + u];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    for (int c = threadIdx.x; c < 2 * j; c += kThreads)
+        partials[(int64_t)c * B + b] =
+            (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
+}
+
+// DCGS2 small dense step (one workgroup).  Columns 0..m-1 of Q are final, column m (= q_j) is the
+// provisional, once-orthogonalised vector; hq = [Q_m^T W q_j ; q_j^T W q_j] = [a ; alpha] and (if
+// hw) hw = [Q_m^T W A q_j ; q_j^T W A q_j] = [b ; b_j].  With r = sqrt(alpha - a.a) the final
+// vector is qbar = (q_j - Q_m a)/r, so
+//   * H row m is corrected in place (delayed re-orthogonalisation of the previous column):
+//       H(0:m, c) += a H(m, c),  H(m, c) *= r   for c < m      (A Q_m = [Q_m qbar] Hbar holds)
+//   * g = Hbar a  (from the old H: g_i = (H a)_i + a_i t, g_m = r t, t = H(m,:) a)
+//   * the CGS coefficients of A qbar = (A q_j - [Q_m qbar] g)/r:
+//       c_i = (b_i - g_i)/r,  c_m = ((b_j - a.b)/r - g_m)/r
+//   * the update f = A qbar - [Q_m qbar] c = (A q_j)/r - Q_m x - qbar y with
+//       x = g/r + c (first m),  y = g_m/r + c_m.
+// coef layout: [x (m) | c (m+1) | rinv, y, r2]; coef[2m+1+0..2].  Without hw only the H correction
+// and r are produced (end-of-factorisation re-orthogonalisation of the last vector).
+__global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __restrict__ hq,
+                                                         const double* __restrict__ hw,
+                                                         double* __restrict__ H, int64_t ldh,
+                                                         double* __restrict__ coef,
+                                                         int* __restrict__ nan_flag) {
+    __shared__ double lds4[4];
+    __shared__ double sc[4];
+    double s = 0.0, p = 0.0, tt = 0.0;
+    for (int i = threadIdx.x; i < m; i += kThreads) {
+        s = fma(hq[i], hq[i], s);
+        if (hw) {
+            p = fma(hq[i], hw[i], p);
+            tt = fma(H[(int64_t)i * ldh + m], hq[i], tt);   // t = H(m, :) a
+        }
+    }
+    s = block_sum(s, lds4);
+    __syncthreads();
+    if (threadIdx.x == 0) sc[0] = s;
+    __syncthreads();
+    p = block_sum(p, lds4);
+    __syncthreads();
+    if (threadIdx.x == 0) sc[1] = p;
+    __syncthreads();
+    tt = block_sum(tt, lds4);
+    __syncthreads();
+    if (threadIdx.x == 0) sc[2] = tt;
+    __syncthreads();
+    const double r2 = hq[m] - sc[0];
+    const double r = sqrt(r2), rinv = 1.0 / r;
+    if (hw) {
+        const double t = sc[2];
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            double ha = 0.0;
+            for (int c = 0; c < m; ++c) ha = fma(H[(int64_t)c * ldh + i], hq[c], ha);
+            const double gi = fma(hq[i], t, ha);
+            const double ci = (hw[i] - gi) * rinv;
+            coef[m + i] = ci;          // c_i
+            coef[i] = fma(gi, rinv, ci);  // x_i
+        }
+        if (threadIdx.x == 0) {
+            const double gm = r * t;
+            const double cm = ((hw[m] - sc[1]) * rinv - gm) * rinv;
+            coef[2 * m] = cm;
+            coef[2 * m + 2] = fma(gm, rinv, cm);  // y
+        }
+    }
+    __syncthreads();  // every read of the old H is done before it is corrected
+    for (int c = threadIdx.x; c < m; c += kThreads) {
+        double* hc = H + (int64_t)c * ldh;
+        const double hr = hc[m];
+        for (int i = 0; i < m; ++i) hc[i] = fma(hq[i], hr, hc[i]);
+        hc[m] = hr * r;
+    }
+    if (threadIdx.x == 0) {
+        coef[2 * m + 1] = rinv;
+        coef[2 * m + 3] = r2;
+        if (!(r2 > 0.0)) atomicOr(nan_flag, 1);   // breakdown: q_j in span(Q_m)
+    }
+}
+
+// DCGS2 update, one read of Q_m (m columns):  qbar = (q_j - Q_m a) * rinv  -> q_j (in place),
+// f = y * rinv - Q_m x - qbar * yc  -> y (in place), optional ||f||_W^2 partial.
+template <int kPairs>
+__global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
+                                                           const double* __restrict__ a,
+                                                           const double* __restrict__ coef,
+                                                           double* __restrict__ qj, double* __restrict__ f,
+                                                           const double* __restrict__ w, int64_t sv,
+                                                           int tiles_per_field, int tiles_w, int tiles_total,
+                                                           int64_t time_off, int do_time,
+                                                           double* __restrict__ partials) {
+    constexpr int kTile = kThreads * kPairs * 2;
+    __shared__ double lds4[4];
+    const double* x = coef;
+    const double rinv = coef[2 * m + 1], yc = coef[2 * m + 2];
+    if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int c = threadIdx.x; c < m; c += 64) {
+            const double qt = Q[time_off + (int64_t)c * ld];
+            s1 = fma(qt, a[c], s1);
+            s2 = fma(qt, x[c], s2);
+        }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (threadIdx.x == 0) {
+            const double qb = (qj[time_off] - s1) * rinv;
+            qj[time_off] = qb;
+            f[time_off] = f[time_off] * rinv - s2 - qb * yc;
+        }
+    }
+    double nrm = 0.0;
+    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 aq[kPairs], af[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            aq[k] = ld2(qj + r0 + k * 2 * kThreads);
+            const double2 fv = ld2(f + r0 + k * 2 * kThreads);
+            af[k] = make_double2(fv.x * rinv, fv.y * rinv);
+        }
+        const double* qb = Q + r0;
+        int c = 0;
+        for (; c + 2 <= m; c += 2) {
+            double2 q[2][kPairs];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const double ac = -a[c + u], xc = -x[c + u];
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    aq[k].x = fma(ac, q[u][k].x, aq[k].x);
+                    aq[k].y = fma(ac, q[u][k].y, aq[k].y);
+                    af[k].x = fma(xc, q[u][k].x, af[k].x);
+                    af[k].y = fma(xc, q[u][k].y, af[k].y);
+                }
+            }
+        }
+        for (; c < m; ++c) {
+            const double ac = -a[c], xc = -x[c];
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
+                aq[k].x = fma(ac, q.x, aq[k].x);
+                aq[k].y = fma(ac, q.y, aq[k].y);
+                af[k].x = fma(xc, q.x, af[k].x);
+                af[k].y = fma(xc, q.y, af[k].y);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
+            af[k].x = fma(-yc, qbv.x, af[k].x);
+            af[k].y = fma(-yc, qbv.y, af[k].y);
+            st2(qj + r0 + k * 2 * kThreads, qbv);
+            st2(f + r0 + k * 2 * kThreads, af[k]);
+        }
+        if (t < tiles_w) {
+            const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 wv = ld2(w + wr + k * 2 * kThreads);
+                nrm = fma(wv.x * af[k].x, af[k].x, nrm);
+                nrm = fma(wv.y * af[k].y, af[k].y, nrm);
+            }
+        }
+    }
+    nrm = block_sum(nrm, lds4);
+    if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+}
+
+// ------------------------------------------------------------------------------------------
 // Arnoldi finish / normalise:  q = f / sqrt(nrm2)  (all rows + time), H column on the device.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_finish(const double* f,  // may alias q (in-place)
@@ -926,7 +1167,7 @@ int nkv_device_info(int* device, int* cu_count, int64_t* hbm_bytes, char* name, 
 size_t nkv_workspace_bytes(const nkv_layout* L, int max_cols) {
     (void)L;
     if (max_cols < 1) max_cols = 1;
-    return kCtrlBytes + (size_t)kMaxBlocks * (size_t)(max_cols + 1) * sizeof(double);
+    return kCtrlBytes + (size_t)kMaxBlocks * (size_t)(2 * max_cols + 2) * sizeof(double);  // 2 RHS (DCGS2)
 }
 
 int nkv_check_status(void* ws, void* stream) {
@@ -1122,6 +1363,95 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, B, hout_dev, tdot ? Q + T : nullptr,
                        L->ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j, const double* x,
+                   const double* y, double* h_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(x, "x"));
+    CHECK(check_ptr(y, "y"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
+    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    hipStream_t st = S(stream);
+    const bool large = use_large_tiles(L);
+    const int P = large ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    const int kTile = kThreads * P * 2;
+    const int tpf = (int)(L->sv / kTile);
+    int bx = kMaxBlocks / L->n_wf;
+    if (bx > tpf) bx = tpf;
+    if (bx < 1) bx = 1;
+    const int B = bx * L->n_wf;
+    double* part = partials_of(ws);
+    if (tpf > 0) {
+        if (large)
+            hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double), st,
+                               Q, L->ld, j, x, y, w, L->sv, tpf, part, B);
+        else
+            hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double),
+                               st, Q, L->ld, j, x, y, w, L->sv, tpf, part, B);
+        NKV_LAUNCHED();
+    }
+    const int64_t T = rows_of(L);
+    const bool tdot = (flags & NKV_TIME) && L->rank0;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, h_dev,
+                       tdot ? Q + T : nullptr, L->ld, tdot ? x + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part + (int64_t)j * B, tpf > 0 ? B : 0,
+                       h_dev + j, tdot ? Q + T : nullptr, L->ld, tdot ? y + T : nullptr, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, double* H_dev, int64_t ldh,
+                   double* coef_dev, void* ws, void* stream) {
+    if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
+    if (!hq_dev || !H_dev || !coef_dev) return fail(NKV_EINVAL, "hq/H/coef is NULL");
+    if (ldh < m + 1) return fail(NKV_EINVAL, "ldh=%lld < m+1=%d", (long long)ldh, m + 1);
+    CHECK(check_ptr(ws, "ws"));
+    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), 0, S(stream), m, hq_dev, hw_dev, H_dev, ldh, coef_dev,
+                       nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* a_dev,
+                     const double* coef_dev, double* qj, double* f, double* nrm2_dev, void* ws, unsigned flags,
+                     void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(qj, "qj"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(ws, "ws"));
+    if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
+    if (!a_dev || !coef_dev || !nrm2_dev) return fail(NKV_EINVAL, "a/coef/nrm2 is NULL");
+    hipStream_t st = S(stream);
+    const bool large = use_large_tiles(L);
+    const int P = large ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    const int kTile = kThreads * P * 2;
+    const int tpf = (int)(L->sv / kTile);
+    const int tiles_w = tpf * L->n_wf;
+    const int tiles_total = (int)(rows_of(L) / kTile);
+    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    if (g < 1) g = 1;
+    const int64_t T = rows_of(L);
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    double* part = partials_of(ws);
+    if (large)
+        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev, coef_dev, qj,
+                           f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    else
+        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS_SMALL>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev,
+                           coef_dev, qj, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    NKV_LAUNCHED();
+    const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev, tdot ? f + T : nullptr,
+                       (int64_t)0, tdot ? f + T : nullptr, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -72,7 +72,7 @@ def get_vec(out: NekVector, X: Basis, coeffs, k: int | None = None) -> None:
 
 
 def eigs(ctx: NekContext, A: LinearOperator, X: Basis, nev: int, tolerance: float, transpose: bool = False,
-         schur_del: float = 0.1, mode: str = "cgs2"):
+         schur_del: float = 0.1, mode: str = "dcgs2"):
     """Leading eigenpairs of A (or A^T) in the caller's basis X (X[0] = prepared seed).  Returns
     (eigvecs[k,k] complex Krylov coefficients, eigvals[k], residuals[k], info)."""
     k = X.k - 1

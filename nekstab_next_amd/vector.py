@@ -71,6 +71,9 @@ class NekContext:
         self.h1 = torch.zeros(max_cols + 1, **f64)
         self.h2 = torch.zeros(max_cols + 1, **f64)
         self.scal = torch.zeros(8, **f64)
+        # DCGS2: [Q^T W q_j ; Q^T W A q_j] (one all-reduce) and the small-step coefficients
+        self.hd = torch.zeros(2 * (max_cols + 1), **f64)
+        self.coef = torch.zeros(2 * max_cols + 8, **f64)
 
     # ---- plumbing ----------------------------------------------------------------------------
     @property
@@ -79,6 +82,10 @@ class NekContext:
 
     def call(self, name: str, *args) -> None:
         _lib.check(getattr(self.lib, name)(self._Lp, *args), name)
+
+    def call_nl(self, name: str, *args) -> None:
+        """Entry points without a layout argument (small dense device kernels)."""
+        _lib.check(getattr(self.lib, name)(*args), name)
 
     def check_nan(self) -> None:
         """Surface a NaN flagged by any reduction so far (synchronises the stream)."""

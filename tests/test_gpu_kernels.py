@@ -233,7 +233,7 @@ def test_rotate_cols_vs_oracle(gpu, k, n_out):
         np.testing.assert_array_equal(syn.to_reference_order(lay, got[i]), Qref[i])
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     lay = LAYOUTS[name]
@@ -338,7 +338,7 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
     np.testing.assert_allclose(hout.cpu().numpy(), href, rtol=1e-12, atol=1e-12 * np.abs(href).max())
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2"])
 def test_arnoldi_with_time_component_vs_oracle(gpu, mode):
     """uparam(1)==2.1: the scalar `time` enters k_dot (krylov_subspace.f90:52-54) and follows every
     update; the operator propagates it (time_scale)."""

@@ -45,7 +45,7 @@ def _seed(ctx, lay, L, w, s=11):
     return seed, q1
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2"])
 def test_config1_krylov_schur(gpu, mode):
     """Config 1: 2-D lx1=6, E=1136 (N=99,968), diag spectrum, k_dim=16, schur_tgt=5."""
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=1136)
@@ -62,7 +62,8 @@ def test_config1_krylov_schur(gpu, mode):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1], exact, atol=1e-9)
 
 
-def test_config2_cylinder_krylov_schur_conjugate_pairs(gpu):
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+def test_config2_cylinder_krylov_schur_conjugate_pairs(gpu, mode):
     """Config 2 (real cylinder mesh size E=1996, N=175,648): rotation-scaling operator with three
     dominant conjugate pairs, k_dim=64, schur_tgt=2 (1cyl.usr:15)."""
     lay = cylinder_layout(1996)
@@ -71,7 +72,7 @@ def test_config2_cylinder_krylov_schur_conjugate_pairs(gpu):
     L = olayout(lay)
     c, s, dr, exact = syn.rot2_operator(lay)
     seed, q1 = _seed(ctx, lay, L, w, 5)
-    cfg = KrylovSchurConfig(k_dim=64, schur_tgt=2)
+    cfg = KrylovSchurConfig(k_dim=64, schur_tgt=2, mode=mode)
     res = krylov_schur(ctx, Rot2Operator(ctx, c, s, dr), seed, cfg)
     ref = orc.krylov_schur(L, w, oracle_rot2_matvec(lay, c, s, dr), q1, 64, 2)
     _compare_ks(res, ref, cfg)
@@ -84,7 +85,8 @@ def test_config2_cylinder_krylov_schur_conjugate_pairs(gpu):
     assert abs(ctx.dot(re, re, False) + ctx.dot(im, im, False) - 1.0) < 1e-12
 
 
-def test_config3_reduced_vs_oracle(gpu):
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+def test_config3_reduced_vs_oracle(gpu, mode):
     """Config 3 operator family at reduced N (3-D lx1=8, E=128: N=289,792), Arnoldi m=64 and
     Krylov–Schur k_dim=32, schur_tgt=4."""
     lay = box3d_layout(128)
@@ -96,7 +98,7 @@ def test_config3_reduced_vs_oracle(gpu):
     orc.set_threads(8)
     try:
         for k, tgt in ((64, 0), (32, 4)):
-            cfg = KrylovSchurConfig(k_dim=k, schur_tgt=tgt)
+            cfg = KrylovSchurConfig(k_dim=k, schur_tgt=tgt, mode=mode)
             res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)
             ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, k, tgt)
             _compare_ks(res, ref, cfg)
@@ -105,7 +107,8 @@ def test_config3_reduced_vs_oracle(gpu):
         orc.set_threads(1)
 
 
-def test_config3_full_size_properties(gpu):
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+def test_config3_full_size_properties(gpu, mode):
     """BASELINE size N=100,014,464, m=128: Ritz values vs the exact spectrum, W-orthonormality of
     the basis and the Arnoldi relation A Q_m = Q_{m+1} H (size-independent checks)."""
     lay = box3d_layout(44176)
@@ -117,7 +120,7 @@ def test_config3_full_size_properties(gpu):
     del d
     seed = ctx.vector()
     seed.fill_hash(11)
-    cfg = KrylovSchurConfig(k_dim=m, schur_tgt=0)
+    cfg = KrylovSchurConfig(k_dim=m, schur_tgt=0, mode=mode)
     res = krylov_schur(ctx, op, seed, cfg)
     np.testing.assert_allclose(res.vals[:8].real, exact[:8], rtol=1e-10)
     Q, H = res.Q, res.H
@@ -174,7 +177,8 @@ def test_config4_gmres_vs_oracle(gpu):
     assert np.max(np.abs(got[:nw] - rref[:nw] / J[:nw])) < 1e-3
 
 
-def test_config5_direct_adjoint_biorthogonal(gpu):
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+def test_config5_direct_adjoint_biorthogonal(gpu, mode):
     """Config 5 (reduced): two Krylov–Schur runs on A = D + rank-2 non-normal term and its
     W-adjoint, two bases resident, then bi-orthogonalisation of the leading pair:
     <adjoint, direct>_W = 1 + 0i to 1e-12; Ritz values vs the oracle to 1e-10."""
@@ -187,7 +191,7 @@ def test_config5_direct_adjoint_biorthogonal(gpu):
     vs = [ctx.vector().from_packed(v) for v in vecs_h]
     A = RankTwoPerturbed(DiagOperator(ctx, d), *vs, sigma=50.0)
     seed, q1 = _seed(ctx, lay, L, w)
-    cfg = KrylovSchurConfig(k_dim=30, schur_tgt=2)
+    cfg = KrylovSchurConfig(k_dim=30, schur_tgt=2, mode=mode)
     rd = krylov_schur(ctx, A, seed, cfg)
     ra = krylov_schur(ctx, A, seed, cfg, transpose=True)
     for tr, res in ((False, rd), (True, ra)):
@@ -207,8 +211,9 @@ def test_config5_direct_adjoint_biorthogonal(gpu):
         np.testing.assert_allclose(syn.to_reference_order(lay, x.to_packed()), y, rtol=1e-12, atol=1e-14)
 
 
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
 @pytest.mark.parametrize("opname", ["diag", "rot2"])
-def test_graph_replay_is_bit_identical(gpu, opname):
+def test_graph_replay_is_bit_identical(gpu, opname, mode):
     """cfg.graphs=True replays captured factorisations: same kernels in the same order, so the
     Krylov–Schur result equals the eager run bit for bit (restarts exercise several mstart graphs)."""
     lay = cylinder_layout(400)
@@ -217,11 +222,11 @@ def test_graph_replay_is_bit_identical(gpu, opname):
     if opname == "diag":
         d, _ = syn.diag_spectrum(lay)
         op = DiagOperator(ctx, d)
-        cfg = dict(k_dim=16, schur_tgt=5)
+        cfg = dict(k_dim=16, schur_tgt=5, mode=mode)
     else:
         c, s, dr, _ = syn.rot2_operator(lay)
         op = Rot2Operator(ctx, c, s, dr)
-        cfg = dict(k_dim=24, schur_tgt=2)
+        cfg = dict(k_dim=24, schur_tgt=2, mode=mode)
     seed = ctx.vector()
     seed.fill_hash(11)
     r1 = krylov_schur(ctx, op, seed, KrylovSchurConfig(**cfg))
