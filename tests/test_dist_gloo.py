@@ -53,6 +53,55 @@ def _cgs2_arnoldi(lay, w, d, q0, m, comm):
     return H
 
 
+def _dcgs2_arnoldi(lay, w, d, q0, m, comm):
+    """Sharded DCGS2 Arnoldi in numpy on one rank, the algebra of nkv_block_dot2 /
+    nkv_dcgs2_coef / nkv_dcgs2_update: ONE all-reduce of [Q^T W q_j ; Q^T W A q_j] (2j values) and
+    one of ||f||^2 per step, the previous column re-orthogonalised with a delay, a closing pass."""
+    wf = np.zeros(lay.ld)
+    for f in range(lay.n_wf):
+        wf[f * lay.sv: f * lay.sv + lay.n_v] = w
+    Q = np.zeros((m + 1, lay.ld))
+    H = np.zeros((m + 1, m))
+    Q[0] = q0
+
+    def correct(mm, a):   # H row mm corrected for q_mm = r qbar + Q_mm a; returns r, old row t-part
+        r = np.sqrt(hq[mm] - a @ a)
+        row = H[mm, :mm].copy()
+        H[:mm, :mm] += np.outer(a, row)
+        H[mm, :mm] = row * r
+        return r, row
+
+    for j in range(1, m + 1):
+        mm = j - 1
+        f = d * Q[mm]
+        h = torch.as_tensor(np.concatenate([Q[:j] @ (wf * Q[mm]), Q[:j] @ (wf * f)]))
+        comm.allreduce_(h)
+        h = h.numpy()
+        hq, hw = h[:j], h[j:]
+        a, b = hq[:mm], hw[:mm]
+        Hold = H[:mm, :mm].copy()
+        r, row = correct(mm, a)
+        t = row @ a
+        g = np.concatenate([Hold @ a + a * t, [r * t]])
+        c = np.concatenate([(b - g[:mm]) / r, [((hw[mm] - a @ b) / r - g[mm]) / r]])
+        x, y = g[:mm] / r + c[:mm], g[mm] / r + c[mm]
+        qbar = (Q[mm] - a @ Q[:mm]) / r
+        Q[mm] = qbar
+        f = f / r - x @ Q[:mm] - qbar * y
+        nrm = torch.as_tensor([np.sum(wf * f * f)])
+        comm.allreduce_(nrm)
+        beta = float(np.sqrt(nrm.item()))
+        H[:j, j - 1] = c
+        H[j, j - 1] = beta
+        Q[j] = f / beta
+    hq = torch.as_tensor(Q[: m + 1] @ (wf * Q[m]))
+    comm.allreduce_(hq)
+    hq = hq.numpy()
+    r, _ = correct(m, hq[:m])
+    Q[m] = (Q[m] - hq[:m] @ Q[:m]) / r
+    return H
+
+
 def _worker(rank, world, port, out):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -77,8 +126,9 @@ def _worker(rank, world, port, out):
         comm.allreduce_(n2)
         q0 = q0 / np.sqrt(n2.item())
         H = _cgs2_arnoldi(lay, w, d, q0, 12, comm)
+        Hd = _dcgs2_arnoldi(lay, w, d, q0, 12, comm)
         mx = comm.max_scalar(float(rank))
-        out[rank] = (H, mx)
+        out[rank] = (H, mx, Hd)
     finally:
         dist.destroy_process_group()
 
@@ -89,9 +139,10 @@ def test_sharded_cgs2_equals_unsharded():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    H0, mx0 = out[0]
-    H1, mx1 = out[1]
+    H0, mx0, Hd0 = out[0]
+    H1, mx1, Hd1 = out[1]
     np.testing.assert_array_equal(H0, H1)  # every rank holds identical (all-reduced) H
+    np.testing.assert_array_equal(Hd0, Hd1)
     assert mx0 == mx1 == 1.0
 
     sys.path.insert(0, ROOT)
@@ -109,6 +160,8 @@ def test_sharded_cgs2_equals_unsharded():
     q0 = q0 / np.sqrt(np.sum(wf * q0 * q0))
     Href = _cgs2_arnoldi(g, w, d, q0, 12, Comm())
     assert np.max(np.abs(H0 - Href)) <= 1e-12 * np.max(np.abs(Href))
+    # DCGS2 (sharded, 2 all-reduces per step) builds the same Arnoldi factorisation as CGS2
+    assert np.max(np.abs(Hd0 - Href)) <= 1e-12 * np.max(np.abs(Href))
 
 
 def _dot_worker(rank, world, port, out):

@@ -8,7 +8,8 @@ import csv
 import json
 import sys
 
-FAM = {"block_dot": "k_block_dot", "update_dot": "k_update_dot", "block_update": "k_block_update<false, true",
+FAM = {"block_dot": "k_block_dot<", "block_dot2": "k_block_dot2<", "dcgs2_update": "k_dcgs2_update<",
+       "update_dot": "k_update_dot", "block_update": "k_block_update<false, true",
        "finish": "k_finish", "op_diag": "k_op_diag"}
 
 

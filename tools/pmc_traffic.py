@@ -16,7 +16,9 @@ import os
 import sys
 
 FAMILIES = {
-    "block_dot": ("k_block_dot",),
+    "block_dot": ("k_block_dot<",),
+    "block_dot2": ("k_block_dot2<",),
+    "dcgs2_update": ("k_dcgs2_update<",),
     "block_update": ("k_block_update",),
     "update_dot": ("k_update_dot",),
     "finish": ("k_finish",),
