@@ -45,6 +45,15 @@ namespace {
 #ifndef NKV_FUSE_G
 #define NKV_FUSE_G 1024  // workgroups of the fused update+dot
 #endif
+#ifndef NKV_DC_PAIRS
+#define NKV_DC_PAIRS 8  // double2 per thread per tile in the DCGS2 kernels (large problems)
+#endif
+#ifndef NKV_DC_U
+#define NKV_DC_U 2  // basis columns in flight in the DCGS2 dual update
+#endif
+#ifndef NKV_D2_U
+#define NKV_D2_U 2  // basis columns in flight in the two-vector multi-dot
+#endif
 #ifndef NKV_FUSE_PF
 #define NKV_FUSE_PF 0  // 1: prefetch the next tile's columns across the per-tile barrier
 #endif
@@ -461,7 +470,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                                                          int tiles_per_field,
                                                          double* __restrict__ partials, int B) {
     constexpr int kTile = kThreads * kPairs * 2;
-    constexpr int U = 2;  // columns in flight (two right-hand sides double the registers per column)
+    constexpr int U = NKV_D2_U;  // columns in flight (two right-hand sides double the registers per column)
     extern __shared__ double red[];  // [4 waves][2j]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
@@ -636,15 +645,16 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
             af[k] = make_double2(fv.x * rinv, fv.y * rinv);
         }
         const double* qb = Q + r0;
+        constexpr int U = NKV_DC_U;
         int c = 0;
-        for (; c + 2 <= m; c += 2) {
-            double2 q[2][kPairs];
+        for (; c + U <= m; c += U) {
+            double2 q[U][kPairs];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const double ac = -a[c + u], xc = -x[c + u];
 #pragma unroll
                 for (int k = 0; k < kPairs; ++k) {
@@ -1379,7 +1389,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
-    const int P = large ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
     const int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
     int bx = kMaxBlocks / L->n_wf;
@@ -1389,7 +1399,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     double* part = partials_of(ws);
     if (tpf > 0) {
         if (large)
-            hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double), st,
+            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double), st,
                                Q, L->ld, j, x, y, w, L->sv, tpf, part, B);
         else
             hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double),
@@ -1432,7 +1442,7 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     if (!a_dev || !coef_dev || !nrm2_dev) return fail(NKV_EINVAL, "a/coef/nrm2 is NULL");
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
-    const int P = large ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
     const int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
     const int tiles_w = tpf * L->n_wf;
@@ -1443,7 +1453,7 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
     if (large)
-        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev, coef_dev, qj,
+        hipLaunchKernelGGL(k_dcgs2_update<NKV_DC_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev, coef_dev, qj,
                            f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
     else
         hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS_SMALL>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev,

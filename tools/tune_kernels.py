@@ -47,6 +47,11 @@ VARIANTS = {
     "rot_w8_nb2": {"NKV_ROT_WAVES": 8, "NKV_ROT_NB": 2},
     "rot_u2": {"NKV_ROT_U": 2},
     "rot_u8": {"NKV_ROT_U": 8},
+    "dc_u4": {"NKV_DC_U": 4},
+    "dc_p4": {"NKV_DC_PAIRS": 4},
+    "dc_p4_u4": {"NKV_DC_PAIRS": 4, "NKV_DC_U": 4, "NKV_D2_U": 4},
+    "d2_u1": {"NKV_D2_U": 1},
+    "dc_nt0": {"NKV_NT": 0},
 }
 
 
@@ -101,6 +106,9 @@ def run(names, E, rounds, js, only=None):
     nrm = torch.zeros(8, dtype=torch.float64, device=dev)
     N, Nw, nv = lay.N, lay.N_w, lay.n_v
     V = torch.eye(jmax, dtype=torch.float64, device=dev).flatten()  # rotation by I keeps Q bounded
+    hd = torch.zeros(2 * (jmax + 1), dtype=torch.float64, device=dev)
+    coef = torch.zeros(2 * jmax + 8, dtype=torch.float64, device=dev)
+    coef.fill_(1.0)   # x = y = rinv = 1: values stay O(1..1e3) over the timed repetitions
 
     def ops(L, j):
         return {
@@ -110,6 +118,13 @@ def run(names, E, rounds, js, only=None):
                             8.0 * (j * N + 2 * N + nv)),
             "update_dot": (lambda: L.nkv_block_update_dot(Lp, w.data_ptr(), Q.data_ptr(), j, h.data_ptr(), f.data_ptr(), h2.data_ptr(), ws.data_ptr(), 0x1, st),
                            8.0 * (j * N + 2 * N + nv)),
+            "dot2": (lambda: L.nkv_block_dot2(Lp, w.data_ptr(), Q.data_ptr(), j, Q[j - 1].data_ptr(), f.data_ptr(),
+                                              hd.data_ptr(), ws.data_ptr(), 0, st),
+                     8.0 * (j * Nw + 2 * Nw + nv)),
+            "dcgs2_update": (lambda: L.nkv_dcgs2_update(Lp, w.data_ptr(), Q.data_ptr(), j - 1, h.data_ptr(), coef.data_ptr(),
+                                                        Q[j - 1].data_ptr(), f.data_ptr(), nrm.data_ptr(), ws.data_ptr(),
+                                                        0x1, st),
+                             8.0 * ((j - 1) * N + 4 * N + nv)),
             "rotate": (lambda: L.nkv_rotate(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, st), 16.0 * j * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
