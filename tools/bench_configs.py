@@ -4,6 +4,7 @@
 config 2: cylinder layout scaled to E=22,728 (N=2,000,064), rotation-scaling operator with
           conjugate pairs, Krylov–Schur k_dim=64, schur_tgt=2 — eager launches vs HIP-graph replay.
 config 4: Newton–Krylov GMRES on J = D - I, cylinder mesh (N=175,648), k_dim=200, tol 1e-9.
+config 5: direct + adjoint Krylov–Schur, N=50,007,232, k_dim=96, two bases resident, + bi-orthogonalisation.
 Prints one JSON object per measurement.
 """
 import json
@@ -34,8 +35,9 @@ def main():
     op = Rot2Operator(ctx, c, s, dr)
     seed = ctx.vector()
     seed.fill_hash(5)
-    for graphs in (False, True, False, True):
-        cfg = KrylovSchurConfig(k_dim=64, schur_tgt=2, graphs=graphs)
+    for mode, graphs in (("cgs2", False), ("dcgs2", False), ("dcgs2", True), ("cgs2", False), ("dcgs2", False),
+                         ("dcgs2", True)):
+        cfg = KrylovSchurConfig(k_dim=64, schur_tgt=2, graphs=graphs, mode=mode)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         r = krylov_schur(ctx, op, seed, cfg)
@@ -44,7 +46,7 @@ def main():
         steps = 64 + sum(64 - (m - 1) for m in r.mstart_history)
         conv = r.residual < 1e-6
         err = max(float(np.min(np.abs(exact - v))) for v in r.vals[conv])
-        print(json.dumps(dict(config="config2", N=lay.N, k_dim=64, graphs=graphs, seconds=round(dt, 4),
+        print(json.dumps(dict(config="config2", N=lay.N, k_dim=64, mode=mode, graphs=graphs, seconds=round(dt, 4),
                               arnoldi_steps=steps, ms_per_step=round(dt / steps * 1e3, 4),
                               restarts=r.schur_cnt, converged=int(conv.sum()), max_err_vs_exact=err)), flush=True)
 
@@ -62,6 +64,46 @@ def main():
         dt = time.perf_counter() - t0
         print(json.dumps(dict(config="config4", N=lay4.N, seconds=round(dt, 4), matvecs=info.matvecs,
                               restarts=info.restarts, final_beta2=info.outer_residuals[-1])), flush=True)
+    del ctx4, op4, rhs, sol
+
+    # config 5 at BASELINE size on ONE GPU (two 97-vector bases = 78 GB resident): direct and
+    # adjoint Krylov–Schur on D + rank-2 non-normal term (k_dim=96, schur_tgt=2), then the
+    # bi-orthogonalisation of the leading pair
+    from nekstab_next_amd.krylov_schur import ritz_vector
+    from nekstab_next_amd.layout import box3d_layout
+    from nekstab_next_amd.operators import RankTwoPerturbed
+    from nekstab_next_amd.sensitivity import biorthogonalize
+
+    lay5 = box3d_layout(22088)
+    ctx5 = NekContext(lay5, weights=syn.mass_weights(lay5), max_cols=97)
+    d5, _ = syn.diag_spectrum(lay5)
+    vs = []
+    for s5 in (21, 22, 23, 24):
+        v = ctx5.vector()
+        v.fill_hash(s5)
+        v.scal(1e-3)
+        vs.append(v)
+    A5 = RankTwoPerturbed(DiagOperator(ctx5, d5), *vs, sigma=50.0)
+    del d5
+    seed5 = ctx5.vector()
+    seed5.fill_hash(11)
+    cfg5 = KrylovSchurConfig(k_dim=96, schur_tgt=2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rd = krylov_schur(ctx5, A5, seed5, cfg5)
+    ra = krylov_schur(ctx5, A5, seed5, cfg5, transpose=True)
+    vecs = [ctx5.vector() for _ in range(4)]
+    ritz_vector(ctx5, rd.Q, rd.vecs, 0, vecs[0], vecs[1], k=96)
+    ritz_vector(ctx5, ra.Q, ra.vecs, 0, vecs[2], vecs[3], k=96)
+    biorthogonalize(ctx5, *vecs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    re = ctx5.dot(vecs[2], vecs[0], False) + ctx5.dot(vecs[3], vecs[1], False)
+    im = ctx5.dot(vecs[2], vecs[1], False) - ctx5.dot(vecs[3], vecs[0], False)
+    print(json.dumps(dict(config="config5", N=lay5.N, k_dim=96, mode=cfg5.mode, seconds=round(dt, 3),
+                          restarts_direct=rd.schur_cnt, restarts_adjoint=ra.schur_cnt,
+                          lambda_direct=str(rd.vals[0]), lambda_adjoint=str(ra.vals[0]),
+                          biorth_re_minus_1=re - 1.0, biorth_im=im)), flush=True)
 
 
 if __name__ == "__main__":
