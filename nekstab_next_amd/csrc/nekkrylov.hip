@@ -51,6 +51,12 @@ namespace {
 #ifndef NKV_DC_U
 #define NKV_DC_U 2  // basis columns in flight in the DCGS2 dual update
 #endif
+#ifndef NKV_DC_FIELDLOOP
+#define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
+#endif
+#ifndef NKV_D2_FIELDLOOP
+#define NKV_D2_FIELDLOOP 1  // two-vector multi-dot: one block walks all weighted fields of a tile
+#endif
 #ifndef NKV_D2_U
 #define NKV_D2_U 2  // basis columns in flight in the two-vector multi-dot
 #endif
@@ -467,58 +473,65 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                                                          int j, const double* __restrict__ x,
                                                          const double* __restrict__ y,
                                                          const double* __restrict__ w, int64_t sv,
-                                                         int tiles_per_field,
+                                                         int tiles_per_field, int n_fields,
                                                          double* __restrict__ partials, int B) {
+    // grid (bx, n_wf / n_fields): each block walks n_fields weighted fields per row tile, so with
+    // n_fields = n_wf the weights of a tile are read from HBM once instead of once per field
     constexpr int kTile = kThreads * kPairs * 2;
     constexpr int U = NKV_D2_U;  // columns in flight (two right-hand sides double the registers per column)
     extern __shared__ double red[];  // [4 waves][2j]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-    const int64_t fb = (int64_t)blockIdx.y * sv;
     for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
-        double2 wx[kPairs], wy[kPairs];
+        double2 wv[kPairs];
 #pragma unroll
-        for (int k = 0; k < kPairs; ++k) {
-            const double2 wv = ld2(w + r0 + k * 2 * kThreads);
-            const double2 xv = ld2(x + fb + r0 + k * 2 * kThreads);
-            const double2 yv = ld2(y + fb + r0 + k * 2 * kThreads);
-            wx[k] = make_double2(wv.x * xv.x, wv.y * xv.y);
-            wy[k] = make_double2(wv.x * yv.x, wv.y * yv.y);
-        }
-        const double* qb = Q + fb + r0;
-        for (int c = 0; c < j; c += U) {
-            double2 q[U][kPairs];
+        for (int k = 0; k < kPairs; ++k) wv[k] = ld2(w + r0 + k * 2 * kThreads);
+        for (int fi = 0; fi < n_fields; ++fi) {
+            const int64_t fb = (int64_t)(blockIdx.y * n_fields + fi) * sv;
+            double2 wx[kPairs], wy[kPairs];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int k = 0; k < kPairs; ++k)
-                    q[u][k] = (c + u < j) ? ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads) : make_double2(0.0, 0.0);
-            double s[2 * U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                double a = 0.0, b = 0.0;
-#pragma unroll
-                for (int k = 0; k < kPairs; ++k) {
-                    a = fma(q[u][k].x, wx[k].x, a);
-                    a = fma(q[u][k].y, wx[k].y, a);
-                    b = fma(q[u][k].x, wy[k].x, b);
-                    b = fma(q[u][k].y, wy[k].y, b);
-                }
-                s[u] = a;
-                s[U + u] = b;
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 xv = ld2(x + fb + r0 + k * 2 * kThreads);
+                const double2 yv = ld2(y + fb + r0 + k * 2 * kThreads);
+                wx[k] = make_double2(wv[k].x * xv.x, wv[k].y * xv.y);
+                wy[k] = make_double2(wv[k].x * yv.x, wv[k].y * yv.y);
             }
+            const double* qb = Q + fb + r0;
+            for (int c = 0; c < j; c += U) {
+                double2 q[U][kPairs];
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1)
+                for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int u = 0; u < 2 * U; ++u) s[u] += __shfl_xor(s[u], off, 64);
-            if (lane == 0) {
+                    for (int k = 0; k < kPairs; ++k)
+                        q[u][k] = (c + u < j) ? ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads)
+                                              : make_double2(0.0, 0.0);
+                double s[2 * U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (c + u < j) {
-                        red[wave * 2 * j + c + u] += s[u];
-                        red[wave * 2 * j + j + c + u] += s[U + u];
+                    double a = 0.0, b = 0.0;
+#pragma unroll
+                    for (int k = 0; k < kPairs; ++k) {
+                        a = fma(q[u][k].x, wx[k].x, a);
+                        a = fma(q[u][k].y, wx[k].y, a);
+                        b = fma(q[u][k].x, wy[k].x, b);
+                        b = fma(q[u][k].y, wy[k].y, b);
+                    }
+                    s[u] = a;
+                    s[U + u] = b;
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+                    for (int u = 0; u < 2 * U; ++u) s[u] += __shfl_xor(s[u], off, 64);
+                if (lane == 0) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (c + u < j) {
+                            red[wave * 2 * j + c + u] += s[u];
+                            red[wave * 2 * j + j + c + u] += s[U + u];
+                        }
                     }
                 }
             }
@@ -606,6 +619,61 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
 
 // DCGS2 update, one read of Q_m (m columns):  qbar = (q_j - Q_m a) * rinv  -> q_j (in place),
 // f = y * rinv - Q_m x - qbar * yc  -> y (in place), optional ||f||_W^2 partial.
+// One row tile (kTile rows at r0): returns f_new in af.
+template <int kPairs>
+__device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t ld, int m,
+                                           const double* __restrict__ a, const double* __restrict__ x,
+                                           double rinv, double yc, double* __restrict__ qj,
+                                           double* __restrict__ f, int64_t r0, double2 (&af)[kPairs]) {
+    double2 aq[kPairs];
+#pragma unroll
+    for (int k = 0; k < kPairs; ++k) {
+        aq[k] = ld2(qj + r0 + k * 2 * kThreads);
+        const double2 fv = ld2(f + r0 + k * 2 * kThreads);
+        af[k] = make_double2(fv.x * rinv, fv.y * rinv);
+    }
+    const double* qb = Q + r0;
+    constexpr int U = NKV_DC_U;
+    int c = 0;
+    for (; c + U <= m; c += U) {
+        double2 q[U][kPairs];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double ac = -a[c + u], xc = -x[c + u];
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                aq[k].x = fma(ac, q[u][k].x, aq[k].x);
+                aq[k].y = fma(ac, q[u][k].y, aq[k].y);
+                af[k].x = fma(xc, q[u][k].x, af[k].x);
+                af[k].y = fma(xc, q[u][k].y, af[k].y);
+            }
+        }
+    }
+    for (; c < m; ++c) {
+        const double ac = -a[c], xc = -x[c];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
+            aq[k].x = fma(ac, q.x, aq[k].x);
+            aq[k].y = fma(ac, q.y, aq[k].y);
+            af[k].x = fma(xc, q.x, af[k].x);
+            af[k].y = fma(xc, q.y, af[k].y);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kPairs; ++k) {
+        const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
+        af[k].x = fma(-yc, qbv.x, af[k].x);
+        af[k].y = fma(-yc, qbv.y, af[k].y);
+        st2(qj + r0 + k * 2 * kThreads, qbv);
+        st2(f + r0 + k * 2 * kThreads, af[k]);
+    }
+}
+
 template <int kPairs>
 __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
                                                            const double* __restrict__ a,
@@ -635,55 +703,35 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
         }
     }
     double nrm = 0.0;
-    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
-        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
-        double2 aq[kPairs], af[kPairs];
+    double2 af[kPairs];
+#if NKV_DC_FIELDLOOP
+    // work unit = one row tile of EVERY weighted field (the norm's weights are read once per unit,
+    // not once per field), then the pressure tiles one by one
+    const int n_wf = tiles_per_field > 0 ? tiles_w / tiles_per_field : 0;
+    const int n_units = tiles_per_field + (tiles_total - tiles_w);
+    for (int u = blockIdx.x; u < n_units; u += gridDim.x) {
+        if (u < tiles_per_field) {
+            double2 wv[kPairs];
 #pragma unroll
-        for (int k = 0; k < kPairs; ++k) {
-            aq[k] = ld2(qj + r0 + k * 2 * kThreads);
-            const double2 fv = ld2(f + r0 + k * 2 * kThreads);
-            af[k] = make_double2(fv.x * rinv, fv.y * rinv);
-        }
-        const double* qb = Q + r0;
-        constexpr int U = NKV_DC_U;
-        int c = 0;
-        for (; c + U <= m; c += U) {
-            double2 q[U][kPairs];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const double ac = -a[c + u], xc = -x[c + u];
+            for (int k = 0; k < kPairs; ++k) wv[k] = ld2(w + (int64_t)u * kTile + 2 * threadIdx.x + k * 2 * kThreads);
+            for (int fi = 0; fi < n_wf; ++fi) {
+                dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f,
+                                   (int64_t)(fi * tiles_per_field + u) * kTile + 2 * threadIdx.x, af);
 #pragma unroll
                 for (int k = 0; k < kPairs; ++k) {
-                    aq[k].x = fma(ac, q[u][k].x, aq[k].x);
-                    aq[k].y = fma(ac, q[u][k].y, aq[k].y);
-                    af[k].x = fma(xc, q[u][k].x, af[k].x);
-                    af[k].y = fma(xc, q[u][k].y, af[k].y);
+                    nrm = fma(wv[k].x * af[k].x, af[k].x, nrm);
+                    nrm = fma(wv[k].y * af[k].y, af[k].y, nrm);
                 }
             }
+        } else {
+            dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f,
+                               (int64_t)(tiles_w + u - tiles_per_field) * kTile + 2 * threadIdx.x, af);
         }
-        for (; c < m; ++c) {
-            const double ac = -a[c], xc = -x[c];
-#pragma unroll
-            for (int k = 0; k < kPairs; ++k) {
-                const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
-                aq[k].x = fma(ac, q.x, aq[k].x);
-                aq[k].y = fma(ac, q.y, aq[k].y);
-                af[k].x = fma(xc, q.x, af[k].x);
-                af[k].y = fma(xc, q.y, af[k].y);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kPairs; ++k) {
-            const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
-            af[k].x = fma(-yc, qbv.x, af[k].x);
-            af[k].y = fma(-yc, qbv.y, af[k].y);
-            st2(qj + r0 + k * 2 * kThreads, qbv);
-            st2(f + r0 + k * 2 * kThreads, af[k]);
-        }
+    }
+#else
+    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f, r0, af);
         if (t < tiles_w) {
             const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
 #pragma unroll
@@ -694,6 +742,7 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
             }
         }
     }
+#endif
     nrm = block_sum(nrm, lds4);
     if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
 }
@@ -1392,18 +1441,21 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
     const int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
-    int bx = kMaxBlocks / L->n_wf;
+    // large problems: one block row walks every field of its tiles (weights read once per tile)
+    const int nf = (large && NKV_D2_FIELDLOOP) ? L->n_wf : 1;
+    const int gy = L->n_wf / nf;
+    int bx = kMaxBlocks / gy;
     if (bx > tpf) bx = tpf;
     if (bx < 1) bx = 1;
-    const int B = bx * L->n_wf;
+    const int B = bx * gy;
     double* part = partials_of(ws);
     if (tpf > 0) {
         if (large)
-            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double), st,
-                               Q, L->ld, j, x, y, w, L->sv, tpf, part, B);
+            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
+                               Q, L->ld, j, x, y, w, L->sv, tpf, nf, part, B);
         else
-            hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, L->n_wf), dim3(kThreads), 8 * j * sizeof(double),
-                               st, Q, L->ld, j, x, y, w, L->sv, tpf, part, B);
+            hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double),
+                               st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, part, B);
         NKV_LAUNCHED();
     }
     const int64_t T = rows_of(L);

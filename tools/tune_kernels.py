@@ -52,6 +52,8 @@ VARIANTS = {
     "dc_p4_u4": {"NKV_DC_PAIRS": 4, "NKV_DC_U": 4, "NKV_D2_U": 4},
     "d2_u1": {"NKV_D2_U": 1},
     "dc_nt0": {"NKV_NT": 0},
+    "d2_nofl": {"NKV_D2_FIELDLOOP": 0},
+    "dc_nofl": {"NKV_DC_FIELDLOOP": 0},
 }
 
 
