@@ -399,3 +399,133 @@ def test_empty_shard(gpu):
     V = torch.eye(4, dtype=torch.float64, device=ctx.device).flatten()
     ctx.call("nkv_rotate", Q.ptr, 4, V.data_ptr(), 4, ctx.stream)
     torch.cuda.synchronize()
+
+
+# ---- DCGS2 entry points, each against numpy on the same inputs (small- and large-tile paths) ----
+from nekstab_next_amd.layout import box3d_layout  # noqa: E402
+
+DC_LAYOUTS = {"small": LAYOUTS["3d_scalar"], "large": box3d_layout(4000)}  # large: >= 2048 4096-row tiles
+
+
+def _wfull(lay, w):
+    wf = np.zeros(lay.ld)
+    for f_ in range(lay.n_wf):
+        wf[f_ * lay.sv: f_ * lay.sv + lay.n_v] = w
+    return wf
+
+
+@pytest.mark.parametrize("name", list(DC_LAYOUTS))
+@pytest.mark.parametrize("j", [1, 7, 33])
+def test_block_dot2_vs_numpy(gpu, name, j):
+    lay = DC_LAYOUTS[name]
+    ctx, w = make_ctx(lay, max_cols=40)
+    Q = ctx.basis(j + 1)
+    for i in range(j):
+        Q[i].fill_hash(500 + i)
+        Q[i].time = 0.02 * i
+    x, y = Q[j], ctx.vector()
+    x.fill_hash(8)
+    y.fill_hash(9)
+    x.time, y.time = 0.3, -0.7
+    h = ctx.hd[: 2 * j]
+    ctx.call("nkv_block_dot2", ctx.w.data_ptr(), Q.ptr, j, x.ptr, y.ptr, h.data_ptr(), ctx.ws.data_ptr(), NKV_TIME,
+             ctx.stream)
+    Qh = Q.storage.cpu().numpy()[:j]
+    wf = _wfull(lay, w)
+    t = lay.time_offset
+    xh, yh = x.to_packed(), y.to_packed()
+    ref = np.concatenate([Qh @ (wf * xh) + Qh[:, t] * xh[t], Qh @ (wf * yh) + Qh[:, t] * yh[t]])
+    np.testing.assert_allclose(h.cpu().numpy(), ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+
+
+def _dcgs2_coef_ref(m, hq, hw, H):
+    """numpy restatement of k_dcgs2_coef (same algebra as tests/test_dist_gloo._dcgs2_arnoldi)."""
+    H = H.copy()
+    a = hq[:m]
+    r2 = hq[m] - a @ a
+    r = np.sqrt(r2)
+    row = H[m, :m].copy()
+    Hold = H[:m, :m].copy()
+    H[:m, :m] += np.outer(a, row)
+    H[m, :m] = row * r
+    out = dict(H=H, r2=r2, rinv=1.0 / r)
+    if hw is not None:
+        b = hw[:m]
+        t = row @ a
+        g = np.concatenate([Hold @ a + a * t, [r * t]])
+        c = np.concatenate([(b - g[:m]) / r, [((hw[m] - a @ b) / r - g[m]) / r]])
+        out.update(c=c, x=g[:m] / r + c[:m], y=g[m] / r + c[m])
+    return out
+
+
+@pytest.mark.parametrize("m", [0, 1, 5, 40])
+@pytest.mark.parametrize("with_hw", [True, False])
+def test_dcgs2_coef_vs_numpy(gpu, m, with_hw):
+    rng = np.random.default_rng(m)
+    k = 48
+    ctx, _ = make_ctx(LAYOUTS["2d"], max_cols=k)
+    H = np.zeros((k + 1, k))
+    H[: m + 1, :m] = np.triu(rng.standard_normal((m + 1, m)), -1)
+    hq = np.concatenate([1e-9 * rng.standard_normal(m), [1.0 + 1e-3]])
+    hw = rng.standard_normal(m + 1)
+    Hd = HessenbergDev(ctx, k)
+    Hd.upload(H)
+    hqd = torch.as_tensor(hq).to(ctx.device)
+    hwd = torch.as_tensor(hw).to(ctx.device)
+    ctx.call_nl("nkv_dcgs2_coef", m, hqd.data_ptr(), hwd.data_ptr() if with_hw else None, Hd.t.data_ptr(), k + 1,
+                ctx.coef.data_ptr(), ctx.ws.data_ptr(), ctx.stream)
+    ref = _dcgs2_coef_ref(m, hq, hw if with_hw else None, H)
+    coef = ctx.coef.cpu().numpy()
+    np.testing.assert_allclose(Hd.download(), ref["H"], rtol=1e-14, atol=1e-14)
+    np.testing.assert_allclose(coef[2 * m + 1], ref["rinv"], rtol=1e-15)
+    np.testing.assert_allclose(coef[2 * m + 3], ref["r2"], rtol=1e-15)
+    if with_hw:
+        np.testing.assert_allclose(coef[:m], ref["x"], rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(coef[m: 2 * m + 1], ref["c"], rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(coef[2 * m + 2], ref["y"], rtol=1e-12, atol=1e-14)
+    ctx.check_nan()
+
+
+def test_dcgs2_coef_flags_breakdown(gpu):
+    """alpha - a.a <= 0 (q_j in the span of the basis) sets the NaN flag."""
+    ctx, _ = make_ctx(LAYOUTS["2d"], max_cols=8)
+    Hd = HessenbergDev(ctx, 8)
+    hq = torch.as_tensor(np.array([1.0, 1.0])).to(ctx.device)   # a = [1], alpha = 1 -> r2 = 0
+    ctx.call_nl("nkv_dcgs2_coef", 1, hq.data_ptr(), hq.data_ptr(), Hd.t.data_ptr(), 9, ctx.coef.data_ptr(),
+                ctx.ws.data_ptr(), ctx.stream)
+    with pytest.raises(NkvNaNError):
+        ctx.check_nan()
+
+
+@pytest.mark.parametrize("name", list(DC_LAYOUTS))
+@pytest.mark.parametrize("m", [0, 1, 6, 31])
+def test_dcgs2_update_vs_numpy(gpu, name, m):
+    lay = DC_LAYOUTS[name]
+    ctx, w = make_ctx(lay, max_cols=40)
+    Q = ctx.basis(m + 1)
+    for i in range(m + 1):
+        Q[i].fill_hash(700 + i)
+        Q[i].time = 0.05 * (i + 1)
+    f = ctx.vector()
+    f.fill_hash(77)
+    f.time = 0.4
+    rng = np.random.default_rng(m)
+    a = rng.standard_normal(m) * 1e-2
+    x = rng.standard_normal(m) * 0.3
+    rinv, yc = 1.0 / 1.0003, 0.27
+    coef = np.zeros(2 * m + 8)
+    coef[:m] = x
+    coef[2 * m + 1], coef[2 * m + 2] = rinv, yc
+    ad = torch.as_tensor(a if m else np.zeros(1)).to(ctx.device)
+    ctx.coef[: coef.size].copy_(torch.as_tensor(coef))
+    Qh = Q.storage.cpu().numpy()
+    fh = f.to_packed()
+    nrm = ctx.scal[3:4]
+    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, m, ad.data_ptr(), ctx.coef.data_ptr(), Q.col_ptr(m), f.ptr,
+             nrm.data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+    qbar = (Qh[m] - a @ Qh[:m]) * rinv          # every row incl. the time slot (NKV_TIME)
+    fref = fh * rinv - x @ Qh[:m] - qbar * yc
+    np.testing.assert_allclose(Q.storage[m].cpu().numpy(), qbar, rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(f.to_packed(), fref, rtol=1e-12, atol=1e-13)
+    wf = _wfull(lay, w)
+    np.testing.assert_allclose(nrm.item(), np.sum(wf * fref * fref), rtol=1e-12)
