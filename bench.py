@@ -293,7 +293,8 @@ def main():
             "config": {
                 "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
                 "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
-                "m": m, "mode": args.mode, "parallelism": f"element-shard x{world} + RCCL allreduce",
+                "m": m, "mode": args.mode, "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
+                                + " allreduce") if world > 1 else "single GPU",
             },
             "roofline": {
                 "bound": "hbm",
