@@ -529,3 +529,37 @@ def test_dcgs2_update_vs_numpy(gpu, name, m):
     np.testing.assert_allclose(f.to_packed(), fref, rtol=1e-12, atol=1e-13)
     wf = _wfull(lay, w)
     np.testing.assert_allclose(nrm.item(), np.sum(wf * fref * fref), rtol=1e-12)
+
+
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+def test_arnoldi_long_vs_oracle(gpu, mode):
+    """m = 300 > 256: the two-pass fallback of the fused cgs2 middle pass, DCGS2's 2j-wide dots and
+    its coefficient kernel at large j, against the reference-order MGS2 oracle."""
+    lay = LAYOUTS["2d"]
+    m = 300
+    ctx, w = make_ctx(lay, max_cols=m + 1)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    Q = ctx.basis(m + 1)
+    q0 = syn.hash_vector(lay, 5)
+    Q[0].from_packed(q0)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, m)
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode=mode)
+    H = Hd.download()
+    Qr = np.zeros((m + 1, L.len))
+    Qr[0] = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, Qr[0])
+    Hr = np.zeros((m + 1, m))
+    dref = syn.to_reference_order(lay, d)
+    orc.set_threads(8)
+    try:
+        orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.0),
+                                  Qr, Hr, 1, m)
+    finally:
+        orc.set_threads(1)
+    assert np.max(np.abs(H - Hr)) <= 1e-11 * np.max(np.abs(Hr)), np.max(np.abs(H - Hr))
+    idx = [0, 1, 150, 299, 300]
+    G = np.array([[ctx.dot(Q[a], Q[b], time=False) for b in idx] for a in idx])
+    assert np.max(np.abs(G - np.eye(len(idx)))) < 1e-12
