@@ -51,6 +51,18 @@ namespace {
 #ifndef NKV_DC_U
 #define NKV_DC_U 2  // basis columns in flight in the DCGS2 dual update
 #endif
+#ifndef NKV_NT_ST
+#define NKV_NT_ST 1  // non-temporal stores of streamed vectors (DCGS2 update, finish, synthetic matvec)
+#endif
+#ifndef NKV_STREAM_UNR
+#define NKV_STREAM_UNR 4  // double2 per thread in flight in the streaming vector kernels
+#endif
+#ifndef NKV_DC_EXPERIMENT
+#define NKV_DC_EXPERIMENT 0
+#endif
+#ifndef NKV_DC_G
+#define NKV_DC_G NKV_MAXB  // workgroups of the DCGS2 dual update
+#endif
 #ifndef NKV_DC_FIELDLOOP
 #define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
 #endif
@@ -65,6 +77,8 @@ namespace {
 #endif
 
 constexpr int kThreads = 256;                       // 4 waves of 64
+constexpr int kStreamUnr = NKV_STREAM_UNR;
+static_assert(NKV_TILE % (2 * kThreads * NKV_STREAM_UNR) == 0, "stream chunk must divide the padding");
 static_assert(NKV_TILE % (kThreads * NKV_PAIRS * 2) == 0, "kernel tile must divide the padding");
 static_assert(NKV_TILE % (kThreads * NKV_PAIRS_SMALL * 2) == 0, "kernel tile must divide the padding");
 constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots per column
@@ -183,6 +197,14 @@ __device__ __forceinline__ double2 ldq(const double* p) {
 #endif
 }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+// Stores of whole streamed vectors (800 MB at N=1e8, never re-read from cache): non-temporal (NKV_NT_ST)
+__device__ __forceinline__ void st2s(double* p, double2 v) {
+#if NKV_NT_ST
+    __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+#else
+    st2(p, v);
+#endif
+}
 
 // ------------------------------------------------------------------------------------------
 // block weighted multi-dot:  partials[c][b] = sum over this block's tiles of q_c . (w f)
@@ -669,8 +691,14 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
         af[k].x = fma(-yc, qbv.x, af[k].x);
         af[k].y = fma(-yc, qbv.y, af[k].y);
-        st2(qj + r0 + k * 2 * kThreads, qbv);
-        st2(f + r0 + k * 2 * kThreads, af[k]);
+#if NKV_DC_EXPERIMENT == 1   // timing experiment only: skip the stores (wrong results)
+        if (af[k].x == 12345.678) {
+#endif
+        st2s(qj + r0 + k * 2 * kThreads, qbv);
+        st2s(f + r0 + k * 2 * kThreads, af[k]);
+#if NKV_DC_EXPERIMENT == 1
+        }
+#endif
     }
 }
 
@@ -760,13 +788,20 @@ __global__ __launch_bounds__(kThreads) void k_finish(const double* f,  // may al
                                                      double* __restrict__ beta_out) {
     const double beta = sqrt(nrm2[0]);
     const double inv = 1.0 / beta;  // k_normalize: inv_alpha = 1/alpha; k_cmult (krylov_subspace.f90:87-90)
-    const int64_t pairs = rows / 2;
-    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs;
-         p += (int64_t)gridDim.x * kThreads) {
-        double2 v = ld2(f + 2 * p);
-        v.x *= inv;
-        v.y *= inv;
-        st2(q + 2 * p, v);
+    // rows is a multiple of NKV_TILE, so whole chunks of kStreamUnr double2 per thread; all loads
+    // of a chunk are issued before its stores (f may alias q)
+    const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
+    for (int64_t ci = blockIdx.x; ci < chunks; ci += gridDim.x) {
+        const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
+        double2 v[kStreamUnr];
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u) v[u] = ld2(f + 2 * (p0 + u * kThreads));
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u) {
+            v[u].x *= inv;
+            v[u].y *= inv;
+            st2s(q + 2 * (p0 + u * kThreads), v[u]);
+        }
     }
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
@@ -1049,11 +1084,18 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
                                                       const double* __restrict__ x,
                                                       double* __restrict__ y, int64_t rows,
                                                       int64_t time_off, double ts) {
-    const int64_t pairs = rows / 2;
-    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs;
-         p += (int64_t)gridDim.x * kThreads) {
-        const double2 dv = ld2(d + 2 * p), xv = ld2(x + 2 * p);
-        st2(y + 2 * p, make_double2(dv.x * xv.x, dv.y * xv.y));
+    const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
+    for (int64_t ci = blockIdx.x; ci < chunks; ci += gridDim.x) {
+        const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
+        double2 dv[kStreamUnr], xv[kStreamUnr];
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u) {
+            dv[u] = ld2(d + 2 * (p0 + u * kThreads));
+            xv[u] = ld2(x + 2 * (p0 + u * kThreads));
+        }
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u)
+            st2s(y + 2 * (p0 + u * kThreads), make_double2(dv[u].x * xv[u].x, dv[u].y * xv[u].y));
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
 }
@@ -1499,7 +1541,8 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int tpf = (int)(L->sv / kTile);
     const int tiles_w = tpf * L->n_wf;
     const int tiles_total = (int)(rows_of(L) / kTile);
-    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    const int gmax = NKV_DC_G < kMaxBlocks ? NKV_DC_G : kMaxBlocks;
+    int g = tiles_total < gmax ? tiles_total : gmax;
     if (g < 1) g = 1;
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;

@@ -54,6 +54,12 @@ VARIANTS = {
     "dc_nt0": {"NKV_NT": 0},
     "d2_nofl": {"NKV_D2_FIELDLOOP": 0},
     "dc_nofl": {"NKV_DC_FIELDLOOP": 0},
+    "ntst0": {"NKV_NT_ST": 0},
+    "unr1_ntst0": {"NKV_NT_ST": 0, "NKV_STREAM_UNR": 1},
+    "unr8": {"NKV_STREAM_UNR": 8},
+    "dc_nostore": {"NKV_DC_EXPERIMENT": 1},
+    "dc_g512": {"NKV_DC_G": 512},
+    "dc_g768": {"NKV_DC_G": 768},
 }
 
 
@@ -109,6 +115,9 @@ def run(names, E, rounds, js, only=None):
     N, Nw, nv = lay.N, lay.N_w, lay.n_v
     V = torch.eye(jmax, dtype=torch.float64, device=dev).flatten()  # rotation by I keeps Q bounded
     hd = torch.zeros(2 * (jmax + 1), dtype=torch.float64, device=dev)
+    f2 = torch.zeros(lay.ld, dtype=torch.float64, device=dev)
+    dgl = torch.full((lay.ld,), 0.5, dtype=torch.float64, device=dev)
+    nrm1 = torch.ones(8, dtype=torch.float64, device=dev)
     coef = torch.zeros(2 * jmax + 8, dtype=torch.float64, device=dev)
     coef.fill_(1.0)   # x = y = rinv = 1: values stay O(1..1e3) over the timed repetitions
 
@@ -127,6 +136,9 @@ def run(names, E, rounds, js, only=None):
                                                         Q[j - 1].data_ptr(), f.data_ptr(), nrm.data_ptr(), ws.data_ptr(),
                                                         0x1, st),
                              8.0 * ((j - 1) * N + 4 * N + nv)),
+            "finish": (lambda: L.nkv_arnoldi_finish(Lp, f.data_ptr(), nrm1.data_ptr(), f2.data_ptr(), 0, None, None,
+                                                    None, 0, st), 16.0 * N),
+            "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
             "rotate": (lambda: L.nkv_rotate(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, st), 16.0 * j * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
