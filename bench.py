@@ -68,7 +68,7 @@ def executed_bytes(N, N_w, n_v, m, mode):
             tot += 8.0 * (j * N_w + 2 * N_w + n_v) + 8.0 * ((j - 1) * N + 4 * N + n_v)
         else:
             raise ValueError(mode)
-        tot += 8.0 * 2 * N + 8.0 * 3 * N
+        tot += (0.0 if mode == "dcgs2" else 8.0 * 2 * N) + 8.0 * 3 * N   # normalise pass (not in dcgs2) + matvec
     if mode == "dcgs2":  # closing re-orthogonalisation of q_{m+1}: dot, update, normalise
         tot += 8.0 * ((m + 1) * N_w + N_w + n_v) + 8.0 * (m * N + 2 * N) + 8.0 * 2 * N
     return tot

@@ -134,23 +134,25 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
                        unsigned flags, void* stream);
 
 /* ---- DCGS2: classical Gram–Schmidt with delayed re-orthogonalisation (two reads of Q per step,
- * two all-reduces).  Same replacement target as the CGS2 entry points above
- * (update_hessenberg_matrix, krylov_decomposition.f90:103-189); the re-orthogonalisation of q_j is
- * folded into step j+1 and the previous H column corrected on the device.  Step j (m = j-1 final
- * columns, Q column m = provisional q_j, f = A q_j):
- *   nkv_block_dot2(Q, j, x=q_j, y=f) -> h[0:j] = Q^T W q_j, h[j:2j] = Q^T W f      (all-reduce 2j)
- *   nkv_dcgs2_coef(m, h, h+j, H, ldh, coef)   (H row m corrected in place; coef = [x | c | rinv, y, r2])
- *   nkv_dcgs2_update(Q, m, a=h, coef, q_j, f) -> q_j final, f projected, ||f||^2  (all-reduce 1)
- *   nkv_arnoldi_finish(f, nrm2, q_{j+1}, j, h1=coef+m, NULL, Hcol j)
- * After the last step: nkv_block_dot(Q, m+1, q_{m+1}), nkv_dcgs2_coef(m, h, NULL, ...),
- * nkv_block_update(Q, m, h, q_{m+1}), nkv_normalize_dev(q_{m+1}, coef+2m+3).
+ * two all-reduces, no separate normalisation pass).  Same replacement target as the CGS2 entry
+ * points above (update_hessenberg_matrix, krylov_decomposition.f90:103-189); the
+ * re-orthogonalisation AND the normalisation of q_j are folded into step j+1, the previous H
+ * column corrected on the device.  Step j (m = j-1 final columns; Q column m holds u = beta q_j,
+ * beta^2 in nrm (NULL at the first step: u is normalised); f = A u):
+ *   nkv_block_dot2(Q, j, x=u, y=f) -> h[0:j] = Q^T W u, h[j:2j] = Q^T W f          (all-reduce 2j)
+ *   nkv_dcgs2_coef(m, h, h+j, nrm, H, ldh, coef)   H(m,m-1) = beta, row m corrected, column m = c;
+ *                                                  coef = [x | c | rinv, y, (beta r)^2, s | a]
+ *   nkv_dcgs2_update(Q, m, coef, u, f, Q col j, nrm) -> column m final, column j = the next u,
+ *                                                  nrm = ||next u||_W^2              (all-reduce 1)
+ * After the last step (m = mend): nkv_block_dot(Q, m+1, u), nkv_dcgs2_coef(m, h, NULL, nrm, ...),
+ * nkv_block_update(Q, m, h, u), nkv_normalize_dev(u, coef+2m+3).
  * H is column-major with leading dimension ldh (>= m+1) in device memory. */
 int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j, const double* x,
                    const double* y, double* h_dev, void* ws, unsigned flags, void* stream);
-int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, double* H_dev, int64_t ldh,
-                   double* coef_dev, void* ws, void* stream);
-int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* a_dev,
-                     const double* coef_dev, double* qj, double* f, double* nrm2_dev, void* ws, unsigned flags,
+int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev, double* H_dev,
+                   int64_t ldh, double* coef_dev, void* ws, void* stream);
+int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* coef_dev,
+                     double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream);
 
 /* ---- Krylov–Schur restart (a10, schur_condensation eigensolvers.f90:421-442) --------------

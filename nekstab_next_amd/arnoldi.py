@@ -20,10 +20,11 @@ Two orthogonalisation modes share the rest of the path:
   CGS2, cf. Świrydowicz et al. 2020, Bielich et al. 2022): step j projects A q_j once against the
   basis while re-orthogonalising the still-provisional q_j in the same pass — one two-vector
   multi-dot over Q (+ one all-reduce of 2j), a small device kernel that corrects the previous H
-  column and derives the coefficients, one update pass over Q that finalises q_j and projects
-  f (+ the ||f||^2 all-reduce).  Two reads of Q per step instead of three; the last vector of a
-  factorisation is re-orthogonalised once at the end, so on return Q and H are exactly an
-  Arnoldi factorisation, as with cgs2.
+  column and derives the coefficients, one update pass over Q that finalises q_j and writes the
+  projected f straight into the next basis column (+ the ||f||^2 all-reduce; f is normalised one
+  step later, inside the same passes).  Two reads of Q per step instead of three, no separate
+  normalisation pass; the last vector of a factorisation is re-orthogonalised and normalised once
+  at the end, so on return Q and H are exactly an Arnoldi factorisation, as with cgs2.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
 
@@ -140,59 +141,56 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         ctx.timer.end("finish", 16.0 * ctx.layout.N)
 
 
-def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector) -> None:
-    """Step j (1-based) of DCGS2 Arnoldi: Q[0:j-1] final, Q[j-1] provisional, f = A Q[j-1].
-    On return Q[j-1] is final, Q[j] provisional, H columns 0..j-2 final and column j-1 provisional."""
+def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool) -> None:
+    """Step j (1-based) of DCGS2 Arnoldi: Q[0:j-1] final, Q[j-1] = u = beta q_j provisional and not
+    yet normalised (beta^2 in ctx.scal[3], unless ``first``: then u is normalised), f = A u.  On
+    return Q[j-1] is final, Q[j] = the next u (its norm^2 in ctx.scal[3]), H columns 0..j-2 final
+    and column j-1 provisional, H(j, j-1) pending."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
     m = j - 1
     h, coef, nrm = ctx.hd[: 2 * j], ctx.coef, ctx.scal[3:4]
-    qj = Q.col_ptr(m)
+    u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot2")
-    ctx.call("nkv_block_dot2", w, Q.ptr, j, qj, f.ptr, h.data_ptr(), ws, tf, st)
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, h.data_ptr(), ws, tf, st)
     if tm:
         tm.end("block_dot2", 8.0 * (j * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), h[j:].data_ptr(), Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws,
-                st)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), h[j:].data_ptr(), None if first else nrm.data_ptr(),
+                Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws, st)
     if tm:
         tm.begin("dcgs2_update")
-    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, h.data_ptr(), coef.data_ptr(), qj, f.ptr, nrm.data_ptr(), ws,
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, coef.data_ptr(), u, f.ptr, Q.col_ptr(j), nrm.data_ptr(), ws,
              NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
     if tm:
         tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N + lay.n_v))
     ctx.comm.allreduce_(nrm)
-    if tm:
-        tm.begin("finish")
-    ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), Q.col_ptr(j), j, coef[m:].data_ptr(), None,
-             Hd.col_ptr(m), 0, st)
-    if tm:
-        tm.end("finish", 16.0 * lay.N)
 
 
 def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
-    """Re-orthogonalise the provisional Q[m] against Q[0:m] and correct H row m (end of a DCGS2
-    factorisation of m steps)."""
+    """Re-orthogonalise and normalise the provisional Q[m] = u against Q[0:m], fill in H(m, m-1)
+    and correct H row m (end of a DCGS2 factorisation of m steps)."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
-    h, coef = ctx.hd[: m + 1], ctx.coef
-    qm = Q.col_ptr(m)
+    h, coef, nrm = ctx.hd[: m + 1], ctx.coef, ctx.scal[3:4]
+    u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot")
-    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, qm, h.data_ptr(), ws, tf, st)
+    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, u, h.data_ptr(), ws, tf, st)
     if tm:
         tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws, st)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, nrm.data_ptr(), Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(),
+                ws, st)
     if tm:
         tm.begin("block_update")
-    ctx.call("nkv_block_update", w, Q.ptr, m, h.data_ptr(), qm, None, ws, NKV_TIME, st)
+    ctx.call("nkv_block_update", w, Q.ptr, m, h.data_ptr(), u, None, ws, NKV_TIME, st)
     if tm:
         tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
-    ctx.call("nkv_normalize_dev", qm, coef[2 * m + 3:].data_ptr(), None, 0, st)
+    ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
 
 
 def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,
@@ -214,7 +212,7 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
         for mstep in range(mstart, mend + 1):
             (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
-            _dcgs2_step(ctx, Q, Hd, mstep, f)
+            _dcgs2_step(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
         _dcgs2_close(ctx, Q, Hd, mend)
         return
     if mode == "dcgs2":

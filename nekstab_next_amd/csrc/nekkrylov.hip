@@ -566,33 +566,44 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
             (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
 }
 
-// DCGS2 small dense step (one workgroup).  Columns 0..m-1 of Q are final, column m (= q_j) is the
-// provisional, once-orthogonalised vector; hq = [Q_m^T W q_j ; q_j^T W q_j] = [a ; alpha] and (if
-// hw) hw = [Q_m^T W A q_j ; q_j^T W A q_j] = [b ; b_j].  With r = sqrt(alpha - a.a) the final
-// vector is qbar = (q_j - Q_m a)/r, so
-//   * H row m is corrected in place (delayed re-orthogonalisation of the previous column):
-//       H(0:m, c) += a H(m, c),  H(m, c) *= r   for c < m      (A Q_m = [Q_m qbar] Hbar holds)
-//   * g = Hbar a  (from the old H: g_i = (H a)_i + a_i t, g_m = r t, t = H(m,:) a)
-//   * the CGS coefficients of A qbar = (A q_j - [Q_m qbar] g)/r:
-//       c_i = (b_i - g_i)/r,  c_m = ((b_j - a.b)/r - g_m)/r
-//   * the update f = A qbar - [Q_m qbar] c = (A q_j)/r - Q_m x - qbar y with
+// DCGS2 small dense step (one workgroup).  Columns 0..m-1 of Q are final; column m holds
+// u = beta q_j, the provisional (once-orthogonalised) vector NOT yet divided by its norm beta
+// (nrm_prev = beta^2 from the previous step's all-reduce; NULL: u = q_j is normalised, beta = 1).
+// hq = [Q_m^T W u ; u^T W u], hw = [Q_m^T W A u ; u^T W A u] (raw); scaled by 1/beta, 1/beta^2
+// they give a, alpha, b, b_j of q_j.  With r = sqrt(alpha - a.a) the final vector is
+// qbar = (q_j - Q_m a)/r, so
+//   * H(m, m-1) = beta (the pending subdiagonal of the previous column) and H row m is corrected
+//     in place (delayed re-orthogonalisation): H(0:m, c) += a H(m, c), H(m, c) *= r, c < m
+//     (then A Q_m = [Q_m qbar] Hbar holds);
+//   * g = Hbar a  (from the old H: g_i = (H a)_i + a_i t, g_m = r t, t = H(m,:) a);
+//   * the CGS coefficients of A qbar = (A q_j - [Q_m qbar] g)/r, written to H column m:
+//       c_i = (b_i - g_i)/r,  c_m = ((b_j - a.b)/r - g_m)/r;
+//   * the update f = A qbar - [Q_m qbar] c = (A u) s/r - Q_m x - qbar y, s = 1/beta, with
 //       x = g/r + c (first m),  y = g_m/r + c_m.
-// coef layout: [x (m) | c (m+1) | rinv, y, r2]; coef[2m+1+0..2].  Without hw only the H correction
-// and r are produced (end-of-factorisation re-orthogonalisation of the last vector).
+// coef layout: [x (m) | c (m+1) | rinv, y, (beta r)^2, s | a (m)].  Without hw only the pending
+// subdiagonal, the H correction, r and a are produced (closing re-orthogonalisation of the last
+// vector: q = (u - Q_m (beta a)) / (beta r)).
 __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __restrict__ hq,
                                                          const double* __restrict__ hw,
+                                                         const double* __restrict__ nrm_prev,
                                                          double* __restrict__ H, int64_t ldh,
                                                          double* __restrict__ coef,
                                                          int* __restrict__ nan_flag) {
     __shared__ double lds4[4];
     __shared__ double sc[4];
+    const bool pend = nrm_prev != nullptr && m > 0;
+    const double beta = nrm_prev ? sqrt(nrm_prev[0]) : 1.0;
+    const double s1 = 1.0 / beta, s2 = s1 * s1;
+    double* ca = coef + 2 * m + 5;
+    // H(m, c) as it stands after the pending subdiagonal is filled in (c < m)
+    auto hrow = [&](int c) { return (pend && c == m - 1) ? beta : H[(int64_t)c * ldh + m]; };
     double s = 0.0, p = 0.0, tt = 0.0;
     for (int i = threadIdx.x; i < m; i += kThreads) {
-        s = fma(hq[i], hq[i], s);
-        if (hw) {
-            p = fma(hq[i], hw[i], p);
-            tt = fma(H[(int64_t)i * ldh + m], hq[i], tt);   // t = H(m, :) a
-        }
+        const double ai = hq[i] * s1;
+        ca[i] = ai;
+        s = fma(ai, ai, s);
+        tt = fma(hrow(i), ai, tt);   // t = H(m, :) a
+        if (hw) p = fma(ai, hw[i] * s1, p);
     }
     s = block_sum(s, lds4);
     __syncthreads();
@@ -606,53 +617,60 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
     __syncthreads();
     if (threadIdx.x == 0) sc[2] = tt;
     __syncthreads();
-    const double r2 = hq[m] - sc[0];
+    const double r2 = hq[m] * s2 - sc[0];
     const double r = sqrt(r2), rinv = 1.0 / r;
+    const double t = sc[2];
     if (hw) {
-        const double t = sc[2];
+        double* hm = H + (int64_t)m * ldh;   // column m (new, provisional)
         for (int i = threadIdx.x; i < m; i += kThreads) {
             double ha = 0.0;
-            for (int c = 0; c < m; ++c) ha = fma(H[(int64_t)c * ldh + i], hq[c], ha);
-            const double gi = fma(hq[i], t, ha);
-            const double ci = (hw[i] - gi) * rinv;
-            coef[m + i] = ci;          // c_i
-            coef[i] = fma(gi, rinv, ci);  // x_i
+            for (int c = 0; c < m; ++c) ha = fma(H[(int64_t)c * ldh + i], hq[c] * s1, ha);
+            const double gi = fma(hq[i] * s1, t, ha);
+            const double ci = (hw[i] * s1 - gi) * rinv;
+            coef[m + i] = ci;               // c_i
+            coef[i] = fma(gi, rinv, ci);    // x_i
+            hm[i] = ci;
         }
         if (threadIdx.x == 0) {
             const double gm = r * t;
-            const double cm = ((hw[m] - sc[1]) * rinv - gm) * rinv;
+            const double cm = ((hw[m] * s2 - sc[1]) * rinv - gm) * rinv;
             coef[2 * m] = cm;
             coef[2 * m + 2] = fma(gm, rinv, cm);  // y
+            hm[m] = cm;
         }
     }
     __syncthreads();  // every read of the old H is done before it is corrected
     for (int c = threadIdx.x; c < m; c += kThreads) {
         double* hc = H + (int64_t)c * ldh;
-        const double hr = hc[m];
-        for (int i = 0; i < m; ++i) hc[i] = fma(hq[i], hr, hc[i]);
+        const double hr = hrow(c);
+        for (int i = 0; i < m; ++i) hc[i] = fma(hq[i] * s1, hr, hc[i]);
         hc[m] = hr * r;
     }
     if (threadIdx.x == 0) {
         coef[2 * m + 1] = rinv;
-        coef[2 * m + 3] = r2;
+        coef[2 * m + 3] = r2 * beta * beta;
+        coef[2 * m + 4] = s1;
         if (!(r2 > 0.0)) atomicOr(nan_flag, 1);   // breakdown: q_j in span(Q_m)
     }
 }
 
-// DCGS2 update, one read of Q_m (m columns):  qbar = (q_j - Q_m a) * rinv  -> q_j (in place),
-// f = y * rinv - Q_m x - qbar * yc  -> y (in place), optional ||f||_W^2 partial.
-// One row tile (kTile rows at r0): returns f_new in af.
+// DCGS2 update, one read of Q_m (m columns):  qbar = (u s - Q_m a) * rinv  -> column m (in place),
+// f = (A u) s rinv - Q_m x - qbar * yc  -> fout (the next column: normalised one step later),
+// ||f||_W^2 partial.  One row tile (kTile rows at r0): returns f in af.
 template <int kPairs>
 __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t ld, int m,
                                            const double* __restrict__ a, const double* __restrict__ x,
-                                           double rinv, double yc, double* __restrict__ qj,
-                                           double* __restrict__ f, int64_t r0, double2 (&af)[kPairs]) {
+                                           double rinv, double yc, double sc, double* __restrict__ qj,
+                                           const double* __restrict__ win, double* __restrict__ f,
+                                           int64_t r0, double2 (&af)[kPairs]) {
     double2 aq[kPairs];
+    const double wsc = sc * rinv;
 #pragma unroll
     for (int k = 0; k < kPairs; ++k) {
-        aq[k] = ld2(qj + r0 + k * 2 * kThreads);
-        const double2 fv = ld2(f + r0 + k * 2 * kThreads);
-        af[k] = make_double2(fv.x * rinv, fv.y * rinv);
+        const double2 uv = ld2(qj + r0 + k * 2 * kThreads);
+        aq[k] = make_double2(uv.x * sc, uv.y * sc);
+        const double2 fv = ld2(win + r0 + k * 2 * kThreads);
+        af[k] = make_double2(fv.x * wsc, fv.y * wsc);
     }
     const double* qb = Q + r0;
     constexpr int U = NKV_DC_U;
@@ -704,9 +722,9 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
 
 template <int kPairs>
 __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
-                                                           const double* __restrict__ a,
                                                            const double* __restrict__ coef,
-                                                           double* __restrict__ qj, double* __restrict__ f,
+                                                           double* __restrict__ qj, const double* __restrict__ win,
+                                                           double* __restrict__ f,
                                                            const double* __restrict__ w, int64_t sv,
                                                            int tiles_per_field, int tiles_w, int tiles_total,
                                                            int64_t time_off, int do_time,
@@ -714,7 +732,8 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
     constexpr int kTile = kThreads * kPairs * 2;
     __shared__ double lds4[4];
     const double* x = coef;
-    const double rinv = coef[2 * m + 1], yc = coef[2 * m + 2];
+    const double* a = coef + 2 * m + 5;
+    const double rinv = coef[2 * m + 1], yc = coef[2 * m + 2], sc = coef[2 * m + 4];
     if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
         double s1 = 0.0, s2 = 0.0;
         for (int c = threadIdx.x; c < m; c += 64) {
@@ -725,9 +744,9 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
         s1 = wave_sum(s1);
         s2 = wave_sum(s2);
         if (threadIdx.x == 0) {
-            const double qb = (qj[time_off] - s1) * rinv;
+            const double qb = (qj[time_off] * sc - s1) * rinv;
             qj[time_off] = qb;
-            f[time_off] = f[time_off] * rinv - s2 - qb * yc;
+            f[time_off] = win[time_off] * (sc * rinv) - s2 - qb * yc;
         }
     }
     double nrm = 0.0;
@@ -743,7 +762,7 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) wv[k] = ld2(w + (int64_t)u * kTile + 2 * threadIdx.x + k * 2 * kThreads);
             for (int fi = 0; fi < n_wf; ++fi) {
-                dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f,
+                dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f,
                                    (int64_t)(fi * tiles_per_field + u) * kTile + 2 * threadIdx.x, af);
 #pragma unroll
                 for (int k = 0; k < kPairs; ++k) {
@@ -752,14 +771,14 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
                 }
             }
         } else {
-            dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f,
+            dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f,
                                (int64_t)(tiles_w + u - tiles_per_field) * kTile + 2 * threadIdx.x, af);
         }
     }
 #else
     for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
-        dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, qj, f, r0, af);
+        dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, r0, af);
         if (t < tiles_w) {
             const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
 #pragma unroll
@@ -1511,29 +1530,30 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     return NKV_OK;
 }
 
-int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, double* H_dev, int64_t ldh,
-                   double* coef_dev, void* ws, void* stream) {
+int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev, double* H_dev,
+                   int64_t ldh, double* coef_dev, void* ws, void* stream) {
     if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
     if (!hq_dev || !H_dev || !coef_dev) return fail(NKV_EINVAL, "hq/H/coef is NULL");
     if (ldh < m + 1) return fail(NKV_EINVAL, "ldh=%lld < m+1=%d", (long long)ldh, m + 1);
     CHECK(check_ptr(ws, "ws"));
-    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), 0, S(stream), m, hq_dev, hw_dev, H_dev, ldh, coef_dev,
-                       nan_flag_of(ws));
+    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), 0, S(stream), m, hq_dev, hw_dev, nrm_prev_dev, H_dev,
+                       ldh, coef_dev, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }
 
-int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* a_dev,
-                     const double* coef_dev, double* qj, double* f, double* nrm2_dev, void* ws, unsigned flags,
+int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* coef_dev,
+                     double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream) {
     CHECK(check_layout(L));
     CHECK(check_ptr(w, "w"));
     CHECK(check_ptr(Q, "Q"));
     CHECK(check_ptr(qj, "qj"));
-    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(win, "win"));
+    CHECK(check_ptr(fout, "fout"));
     CHECK(check_ptr(ws, "ws"));
     if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
-    if (!a_dev || !coef_dev || !nrm2_dev) return fail(NKV_EINVAL, "a/coef/nrm2 is NULL");
+    if (!coef_dev || !nrm2_dev) return fail(NKV_EINVAL, "coef/nrm2 is NULL");
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
     const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
@@ -1548,15 +1568,15 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
     if (large)
-        hipLaunchKernelGGL(k_dcgs2_update<NKV_DC_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev, coef_dev, qj,
-                           f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+        hipLaunchKernelGGL(k_dcgs2_update<NKV_DC_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
+                           win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
     else
-        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS_SMALL>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, a_dev,
-                           coef_dev, qj, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS_SMALL>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
+                           win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
     NKV_LAUNCHED();
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
-    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev, tdot ? f + T : nullptr,
-                       (int64_t)0, tdot ? f + T : nullptr, nan_flag_of(ws));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev, tdot ? fout + T : nullptr,
+                       (int64_t)0, tdot ? fout + T : nullptr, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }

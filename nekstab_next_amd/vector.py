@@ -73,7 +73,7 @@ class NekContext:
         self.scal = torch.zeros(8, **f64)
         # DCGS2: [Q^T W q_j ; Q^T W A q_j] (one all-reduce) and the small-step coefficients
         self.hd = torch.zeros(2 * (max_cols + 1), **f64)
-        self.coef = torch.zeros(2 * max_cols + 8, **f64)
+        self.coef = torch.zeros(3 * max_cols + 8, **f64)
 
     # ---- plumbing ----------------------------------------------------------------------------
     @property

@@ -438,47 +438,58 @@ def test_block_dot2_vs_numpy(gpu, name, j):
     np.testing.assert_allclose(h.cpu().numpy(), ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
 
 
-def _dcgs2_coef_ref(m, hq, hw, H):
-    """numpy restatement of k_dcgs2_coef (same algebra as tests/test_dist_gloo._dcgs2_arnoldi)."""
+def _dcgs2_coef_ref(m, hq, hw, H, beta=None):
+    """numpy restatement of k_dcgs2_coef (same algebra as tests/test_dist_gloo._dcgs2_arnoldi):
+    raw dots of u = beta q_j, pending subdiagonal H(m, m-1) = beta."""
     H = H.copy()
-    a = hq[:m]
-    r2 = hq[m] - a @ a
+    b_ = 1.0 if beta is None else beta
+    if beta is not None and m > 0:
+        H[m, m - 1] = beta
+    a = hq[:m] / b_
+    r2 = hq[m] / b_ ** 2 - a @ a
     r = np.sqrt(r2)
     row = H[m, :m].copy()
     Hold = H[:m, :m].copy()
     H[:m, :m] += np.outer(a, row)
     H[m, :m] = row * r
-    out = dict(H=H, r2=r2, rinv=1.0 / r)
+    out = dict(H=H, r2s=r2 * b_ ** 2, rinv=1.0 / r, a=a, s=1.0 / b_)
     if hw is not None:
-        b = hw[:m]
+        b = hw[:m] / b_
         t = row @ a
         g = np.concatenate([Hold @ a + a * t, [r * t]])
-        c = np.concatenate([(b - g[:m]) / r, [((hw[m] - a @ b) / r - g[m]) / r]])
-        out.update(c=c, x=g[:m] / r + c[:m], y=g[m] / r + c[m])
+        c = np.concatenate([(b - g[:m]) / r, [((hw[m] / b_ ** 2 - a @ b) / r - g[m]) / r]])
+        H[: m + 1, m] = c
+        out.update(H=H, c=c, x=g[:m] / r + c[:m], y=g[m] / r + c[m])
     return out
 
 
 @pytest.mark.parametrize("m", [0, 1, 5, 40])
 @pytest.mark.parametrize("with_hw", [True, False])
-def test_dcgs2_coef_vs_numpy(gpu, m, with_hw):
+@pytest.mark.parametrize("beta", [None, 1.3])
+def test_dcgs2_coef_vs_numpy(gpu, m, with_hw, beta):
     rng = np.random.default_rng(m)
     k = 48
     ctx, _ = make_ctx(LAYOUTS["2d"], max_cols=k)
     H = np.zeros((k + 1, k))
     H[: m + 1, :m] = np.triu(rng.standard_normal((m + 1, m)), -1)
-    hq = np.concatenate([1e-9 * rng.standard_normal(m), [1.0 + 1e-3]])
+    b_ = 1.0 if beta is None else beta
+    hq = np.concatenate([1e-9 * rng.standard_normal(m) * b_, [(1.0 + 1e-3) * b_ ** 2]])
     hw = rng.standard_normal(m + 1)
     Hd = HessenbergDev(ctx, k)
     Hd.upload(H)
     hqd = torch.as_tensor(hq).to(ctx.device)
     hwd = torch.as_tensor(hw).to(ctx.device)
-    ctx.call_nl("nkv_dcgs2_coef", m, hqd.data_ptr(), hwd.data_ptr() if with_hw else None, Hd.t.data_ptr(), k + 1,
-                ctx.coef.data_ptr(), ctx.ws.data_ptr(), ctx.stream)
-    ref = _dcgs2_coef_ref(m, hq, hw if with_hw else None, H)
+    nrm = torch.tensor([b_ ** 2], dtype=torch.float64, device=ctx.device)
+    ctx.call_nl("nkv_dcgs2_coef", m, hqd.data_ptr(), hwd.data_ptr() if with_hw else None,
+                None if beta is None else nrm.data_ptr(), Hd.t.data_ptr(), k + 1, ctx.coef.data_ptr(),
+                ctx.ws.data_ptr(), ctx.stream)
+    ref = _dcgs2_coef_ref(m, hq, hw if with_hw else None, H, beta)
     coef = ctx.coef.cpu().numpy()
-    np.testing.assert_allclose(Hd.download(), ref["H"], rtol=1e-14, atol=1e-14)
-    np.testing.assert_allclose(coef[2 * m + 1], ref["rinv"], rtol=1e-15)
-    np.testing.assert_allclose(coef[2 * m + 3], ref["r2"], rtol=1e-15)
+    np.testing.assert_allclose(Hd.download(), ref["H"], rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(coef[2 * m + 1], ref["rinv"], rtol=1e-14)
+    np.testing.assert_allclose(coef[2 * m + 3], ref["r2s"], rtol=1e-14)
+    np.testing.assert_allclose(coef[2 * m + 4], ref["s"], rtol=1e-15)
+    np.testing.assert_allclose(coef[2 * m + 5: 3 * m + 5], ref["a"], rtol=1e-14, atol=1e-30)
     if with_hw:
         np.testing.assert_allclose(coef[:m], ref["x"], rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(coef[m: 2 * m + 1], ref["c"], rtol=1e-12, atol=1e-14)
@@ -491,7 +502,7 @@ def test_dcgs2_coef_flags_breakdown(gpu):
     ctx, _ = make_ctx(LAYOUTS["2d"], max_cols=8)
     Hd = HessenbergDev(ctx, 8)
     hq = torch.as_tensor(np.array([1.0, 1.0])).to(ctx.device)   # a = [1], alpha = 1 -> r2 = 0
-    ctx.call_nl("nkv_dcgs2_coef", 1, hq.data_ptr(), hq.data_ptr(), Hd.t.data_ptr(), 9, ctx.coef.data_ptr(),
+    ctx.call_nl("nkv_dcgs2_coef", 1, hq.data_ptr(), hq.data_ptr(), None, Hd.t.data_ptr(), 9, ctx.coef.data_ptr(),
                 ctx.ws.data_ptr(), ctx.stream)
     with pytest.raises(NkvNaNError):
         ctx.check_nan()
@@ -502,7 +513,7 @@ def test_dcgs2_coef_flags_breakdown(gpu):
 def test_dcgs2_update_vs_numpy(gpu, name, m):
     lay = DC_LAYOUTS[name]
     ctx, w = make_ctx(lay, max_cols=40)
-    Q = ctx.basis(m + 1)
+    Q = ctx.basis(m + 2)
     for i in range(m + 1):
         Q[i].fill_hash(700 + i)
         Q[i].time = 0.05 * (i + 1)
@@ -512,21 +523,22 @@ def test_dcgs2_update_vs_numpy(gpu, name, m):
     rng = np.random.default_rng(m)
     a = rng.standard_normal(m) * 1e-2
     x = rng.standard_normal(m) * 0.3
-    rinv, yc = 1.0 / 1.0003, 0.27
-    coef = np.zeros(2 * m + 8)
+    rinv, yc, sc = 1.0 / 1.0003, 0.27, 1.0 / 1.7
+    coef = np.zeros(3 * m + 8)
     coef[:m] = x
-    coef[2 * m + 1], coef[2 * m + 2] = rinv, yc
-    ad = torch.as_tensor(a if m else np.zeros(1)).to(ctx.device)
+    coef[2 * m + 1], coef[2 * m + 2], coef[2 * m + 4] = rinv, yc, sc
+    coef[2 * m + 5: 3 * m + 5] = a
     ctx.coef[: coef.size].copy_(torch.as_tensor(coef))
     Qh = Q.storage.cpu().numpy()
     fh = f.to_packed()
     nrm = ctx.scal[3:4]
-    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, m, ad.data_ptr(), ctx.coef.data_ptr(), Q.col_ptr(m), f.ptr,
-             nrm.data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
-    qbar = (Qh[m] - a @ Qh[:m]) * rinv          # every row incl. the time slot (NKV_TIME)
-    fref = fh * rinv - x @ Qh[:m] - qbar * yc
+    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, m, ctx.coef.data_ptr(), Q.col_ptr(m), f.ptr,
+             Q.col_ptr(m + 1), nrm.data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+    qbar = (Qh[m] * sc - a @ Qh[:m]) * rinv          # every row incl. the time slot (NKV_TIME)
+    fref = fh * sc * rinv - x @ Qh[:m] - qbar * yc
     np.testing.assert_allclose(Q.storage[m].cpu().numpy(), qbar, rtol=1e-12, atol=1e-13)
-    np.testing.assert_allclose(f.to_packed(), fref, rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(Q.storage[m + 1].cpu().numpy(), fref, rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(f.to_packed(), fh)   # the matvec output is only read
     wf = _wfull(lay, w)
     np.testing.assert_allclose(nrm.item(), np.sum(wf * fref * fref), rtol=1e-12)
 
