@@ -55,50 +55,55 @@ def _cgs2_arnoldi(lay, w, d, q0, m, comm):
 
 def _dcgs2_arnoldi(lay, w, d, q0, m, comm):
     """Sharded DCGS2 Arnoldi in numpy on one rank, the algebra of nkv_block_dot2 /
-    nkv_dcgs2_coef / nkv_dcgs2_update: ONE all-reduce of [Q^T W q_j ; Q^T W A q_j] (2j values) and
-    one of ||f||^2 per step, the previous column re-orthogonalised with a delay, a closing pass."""
+    nkv_dcgs2_coef / nkv_dcgs2_update with deferred normalisation: ONE all-reduce of
+    [Q^T W u ; Q^T W A u] (2j values) and one of ||f||^2 per step; column j holds u = beta q_j until
+    step j+1 divides the raw dots by beta, corrects H and finalises it; a closing pass at the end."""
     wf = np.zeros(lay.ld)
     for f in range(lay.n_wf):
         wf[f * lay.sv: f * lay.sv + lay.n_v] = w
     Q = np.zeros((m + 1, lay.ld))
     H = np.zeros((m + 1, m))
     Q[0] = q0
+    beta = None
 
-    def correct(mm, a):   # H row mm corrected for q_mm = r qbar + Q_mm a; returns r, old row t-part
-        r = np.sqrt(hq[mm] - a @ a)
+    def correct(mm, hq, beta):   # pending H(mm, mm-1) = beta, row mm corrected for q = r qbar + Q a
+        s = 1.0 if beta is None else 1.0 / beta
+        if beta is not None and mm > 0:
+            H[mm, mm - 1] = beta
+        a = hq[:mm] * s
+        r = np.sqrt(hq[mm] * s * s - a @ a)
         row = H[mm, :mm].copy()
+        Hold = H[:mm, :mm].copy()
         H[:mm, :mm] += np.outer(a, row)
         H[mm, :mm] = row * r
-        return r, row
+        return a, r, row, Hold, s
 
     for j in range(1, m + 1):
         mm = j - 1
-        f = d * Q[mm]
+        f = d * Q[mm]                                   # A u
         h = torch.as_tensor(np.concatenate([Q[:j] @ (wf * Q[mm]), Q[:j] @ (wf * f)]))
         comm.allreduce_(h)
         h = h.numpy()
-        hq, hw = h[:j], h[j:]
-        a, b = hq[:mm], hw[:mm]
-        Hold = H[:mm, :mm].copy()
-        r, row = correct(mm, a)
+        a, r, row, Hold, s = correct(mm, h[:j], beta)
+        b, bj = h[j: j + mm] * s, h[j + mm] * s * s
         t = row @ a
         g = np.concatenate([Hold @ a + a * t, [r * t]])
-        c = np.concatenate([(b - g[:mm]) / r, [((hw[mm] - a @ b) / r - g[mm]) / r]])
+        c = np.concatenate([(b - g[:mm]) / r, [((bj - a @ b) / r - g[mm]) / r]])
         x, y = g[:mm] / r + c[:mm], g[mm] / r + c[mm]
-        qbar = (Q[mm] - a @ Q[:mm]) / r
+        qbar = (Q[mm] * s - a @ Q[:mm]) / r
         Q[mm] = qbar
-        f = f / r - x @ Q[:mm] - qbar * y
-        nrm = torch.as_tensor([np.sum(wf * f * f)])
+        u = f * s / r - x @ Q[:mm] - qbar * y
+        nrm = torch.as_tensor([np.sum(wf * u * u)])
         comm.allreduce_(nrm)
         beta = float(np.sqrt(nrm.item()))
         H[:j, j - 1] = c
-        H[j, j - 1] = beta
-        Q[j] = f / beta
+        Q[j] = u
     hq = torch.as_tensor(Q[: m + 1] @ (wf * Q[m]))
     comm.allreduce_(hq)
     hq = hq.numpy()
-    r, _ = correct(m, hq[:m])
-    Q[m] = (Q[m] - hq[:m] @ Q[:m]) / r
+    correct(m, hq, beta)
+    r2s = hq[m] - (hq[:m] / beta) @ (hq[:m] / beta) * beta * beta
+    Q[m] = (Q[m] - hq[:m] @ Q[:m]) / np.sqrt(r2s)
     return H
 
 
