@@ -66,6 +66,7 @@ extern "C" {
 #define NKV_OVERWRITE 0x4u  /* block_update: f <- + Q h     (k_matmul, krylov_subspace.f90:163)    */
 #define NKV_NORM2 0x8u      /* block_update: also write the local ||f||_W^2 partial               */
 #define NKV_TIME_DOT 0x10u  /* block_update_dot: include the time product in the dot partial      */
+#define NKV_X_IS_LAST 0x20u /* block_dot2: x is column j-1 of Q (its two dots come from registers)  */
 
 typedef struct nkv_layout {
     int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */

@@ -24,6 +24,7 @@ NKV_ACCUMULATE = 0x2
 NKV_OVERWRITE = 0x4
 NKV_NORM2 = 0x8
 NKV_TIME_DOT = 0x10
+NKV_X_IS_LAST = 0x20
 
 
 class NkvError(RuntimeError):

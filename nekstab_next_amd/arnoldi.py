@@ -35,7 +35,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import NKV_NORM2, NKV_TIME, NKV_TIME_DOT
+from ._lib import NKV_NORM2, NKV_TIME, NKV_TIME_DOT, NKV_X_IS_LAST
 from .operators import LinearOperator
 from .vector import Basis, NekContext, NekVector
 
@@ -154,9 +154,9 @@ def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVect
     u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot2")
-    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, h.data_ptr(), ws, tf, st)
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, h.data_ptr(), ws, tf | NKV_X_IS_LAST, st)
     if tm:
-        tm.end("block_dot2", 8.0 * (j * lay.N_w + 2 * lay.N_w + lay.n_v))
+        tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
     ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), h[j:].data_ptr(), None if first else nrm.data_ptr(),
                 Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws, st)

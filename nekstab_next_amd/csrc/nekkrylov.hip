@@ -495,10 +495,12 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                                                          int j, const double* __restrict__ x,
                                                          const double* __restrict__ y,
                                                          const double* __restrict__ w, int64_t sv,
-                                                         int tiles_per_field, int n_fields,
+                                                         int tiles_per_field, int n_fields, int x_last,
                                                          double* __restrict__ partials, int B) {
     // grid (bx, n_wf / n_fields): each block walks n_fields weighted fields per row tile, so with
-    // n_fields = n_wf the weights of a tile are read from HBM once instead of once per field
+    // n_fields = n_wf the weights of a tile are read from HBM once instead of once per field.
+    // x_last: x IS column j-1 of Q, so that column is not streamed again — its two dots (x.Wx,
+    // x.Wy) are formed from the registers that hold x and y.
     constexpr int kTile = kThreads * kPairs * 2;
     constexpr int U = NKV_D2_U;  // columns in flight (two right-hand sides double the registers per column)
     extern __shared__ double red[];  // [4 waves][2j]
@@ -513,22 +515,38 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
         for (int fi = 0; fi < n_fields; ++fi) {
             const int64_t fb = (int64_t)(blockIdx.y * n_fields + fi) * sv;
             double2 wx[kPairs], wy[kPairs];
+            double sxx = 0.0, sxy = 0.0;
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) {
                 const double2 xv = ld2(x + fb + r0 + k * 2 * kThreads);
                 const double2 yv = ld2(y + fb + r0 + k * 2 * kThreads);
                 wx[k] = make_double2(wv[k].x * xv.x, wv[k].y * xv.y);
                 wy[k] = make_double2(wv[k].x * yv.x, wv[k].y * yv.y);
+                if (x_last) {
+                    sxx = fma(xv.x, wx[k].x, sxx);
+                    sxx = fma(xv.y, wx[k].y, sxx);
+                    sxy = fma(xv.x, wy[k].x, sxy);
+                    sxy = fma(xv.y, wy[k].y, sxy);
+                }
             }
+            if (x_last) {
+                sxx = wave_sum(sxx);
+                sxy = wave_sum(sxy);
+                if (lane == 0) {
+                    red[wave * 2 * j + j - 1] += sxx;
+                    red[wave * 2 * j + 2 * j - 1] += sxy;
+                }
+            }
+            const int jl = x_last ? j - 1 : j;   // columns streamed from Q
             const double* qb = Q + fb + r0;
-            for (int c = 0; c < j; c += U) {
+            for (int c = 0; c < jl; c += U) {
                 double2 q[U][kPairs];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
 #pragma unroll
                     for (int k = 0; k < kPairs; ++k)
-                        q[u][k] = (c + u < j) ? ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads)
-                                              : make_double2(0.0, 0.0);
+                        q[u][k] = (c + u < jl) ? ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads)
+                                               : make_double2(0.0, 0.0);
                 double s[2 * U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -550,7 +568,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                 if (lane == 0) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        if (c + u < j) {
+                        if (c + u < jl) {
                             red[wave * 2 * j + c + u] += s[u];
                             red[wave * 2 * j + j + c + u] += s[U + u];
                         }
@@ -1497,6 +1515,8 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     CHECK(check_ptr(ws, "ws"));
     if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
     if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    if ((flags & NKV_X_IS_LAST) && x != Q + (int64_t)(j - 1) * L->ld)
+        return fail(NKV_EINVAL, "NKV_X_IS_LAST: x is not column j-1 of Q");
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
     const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
@@ -1511,12 +1531,13 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     const int B = bx * gy;
     double* part = partials_of(ws);
     if (tpf > 0) {
+        const int xl = (flags & NKV_X_IS_LAST) ? 1 : 0;
         if (large)
             hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
-                               Q, L->ld, j, x, y, w, L->sv, tpf, nf, part, B);
+                               Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
         else
             hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double),
-                               st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, part, B);
+                               st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
         NKV_LAUNCHED();
     }
     const int64_t T = rows_of(L);

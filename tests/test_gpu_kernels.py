@@ -13,7 +13,7 @@ import torch
 import oracle as orc
 from helpers import olayout
 from nekstab_next_amd import synthetic as syn
-from nekstab_next_amd._lib import NKV_NORM2, NKV_OVERWRITE, NKV_TIME, NkvNaNError
+from nekstab_next_amd._lib import NKV_NORM2, NKV_OVERWRITE, NKV_TIME, NkvError, NkvNaNError
 from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
 from nekstab_next_amd.layout import NekLayout
 from nekstab_next_amd.operators import DiagOperator, Rot2Operator
@@ -415,27 +415,33 @@ def _wfull(lay, w):
 
 
 @pytest.mark.parametrize("name", list(DC_LAYOUTS))
-@pytest.mark.parametrize("j", [1, 7, 33])
-def test_block_dot2_vs_numpy(gpu, name, j):
+@pytest.mark.parametrize("j", [1, 2, 7, 33])
+@pytest.mark.parametrize("x_last", [False, True])
+def test_block_dot2_vs_numpy(gpu, name, j, x_last):
+    from nekstab_next_amd._lib import NKV_X_IS_LAST
     lay = DC_LAYOUTS[name]
     ctx, w = make_ctx(lay, max_cols=40)
     Q = ctx.basis(j + 1)
     for i in range(j):
         Q[i].fill_hash(500 + i)
         Q[i].time = 0.02 * i
-    x, y = Q[j], ctx.vector()
+    x, y = (Q[j - 1] if x_last else Q[j]), ctx.vector()
     x.fill_hash(8)
     y.fill_hash(9)
     x.time, y.time = 0.3, -0.7
     h = ctx.hd[: 2 * j]
-    ctx.call("nkv_block_dot2", ctx.w.data_ptr(), Q.ptr, j, x.ptr, y.ptr, h.data_ptr(), ctx.ws.data_ptr(), NKV_TIME,
-             ctx.stream)
+    ctx.call("nkv_block_dot2", ctx.w.data_ptr(), Q.ptr, j, x.ptr, y.ptr, h.data_ptr(), ctx.ws.data_ptr(),
+             NKV_TIME | (NKV_X_IS_LAST if x_last else 0), ctx.stream)
     Qh = Q.storage.cpu().numpy()[:j]
     wf = _wfull(lay, w)
     t = lay.time_offset
     xh, yh = x.to_packed(), y.to_packed()
     ref = np.concatenate([Qh @ (wf * xh) + Qh[:, t] * xh[t], Qh @ (wf * yh) + Qh[:, t] * yh[t]])
     np.testing.assert_allclose(h.cpu().numpy(), ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    if not x_last and j > 1:   # the flag is refused when x is not column j-1
+        with pytest.raises(NkvError):
+            ctx.call("nkv_block_dot2", ctx.w.data_ptr(), Q.ptr, j, x.ptr, y.ptr, h.data_ptr(), ctx.ws.data_ptr(),
+                     NKV_X_IS_LAST, ctx.stream)
 
 
 def _dcgs2_coef_ref(m, hq, hw, H, beta=None):

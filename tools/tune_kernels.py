@@ -135,8 +135,9 @@ def run(names, E, rounds, js, only=None):
             "update_dot": (lambda: L.nkv_block_update_dot(Lp, w.data_ptr(), Q.data_ptr(), j, h.data_ptr(), f.data_ptr(), h2.data_ptr(), ws.data_ptr(), 0x1, st),
                            8.0 * (j * N + 2 * N + nv)),
             "dot2": (lambda: L.nkv_block_dot2(Lp, w.data_ptr(), Q.data_ptr(), j, Q[j - 1].data_ptr(), f.data_ptr(),
-                                              hd.data_ptr(), ws.data_ptr(), 0, st),
-                     8.0 * (j * Nw + 2 * Nw + nv)),
+                                              hd.data_ptr(), ws.data_ptr(), 0x20 if hasattr(L, "nkv_dcgs2_coef") else 0,
+                                              st),
+                     8.0 * ((j - 1) * Nw + 2 * Nw + nv)),
             "dcgs2_update": (lambda: L.nkv_dcgs2_update(Lp, w.data_ptr(), Q.data_ptr(), j - 1, coefs[j].data_ptr(),
                                                         Q[j - 1].data_ptr(), f.data_ptr(), f2.data_ptr(), nrm.data_ptr(),
                                                         ws.data_ptr(), 0x1, st),
