@@ -863,45 +863,39 @@ __global__ __launch_bounds__(kThreads) void k_blas1(double* x, const double* y, 
                                                     const double* __restrict__ a_dev, int64_t rows,
                                                     int64_t time_off, int do_time) {
     if (OP == OP_AXPY_DEV) a = b * a_dev[0];
-    const int64_t pairs = rows / 2;
-    const int64_t n = do_time ? pairs + 1 : pairs;  // last "pair" index = the time slot
-    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n;
-         p += (int64_t)gridDim.x * kThreads) {
-        if (p == pairs) {  // scalar time component
-            const int64_t i = time_off;
-            if (OP == OP_ZERO) x[i] = 0.0;
-            if (OP == OP_COPY) x[i] = y[i];
-            if (OP == OP_SCAL) x[i] = x[i] * a;
-            if (OP == OP_AXPBY) x[i] = x[i] * a + y[i] * b;
-            if (OP == OP_SUB3) x[i] = y[i] - z[i];
-            if (OP == OP_AXPY_DEV) x[i] = fma(a, y[i], x[i]);
-            continue;
+    // rows is a multiple of NKV_TILE: whole chunks of kStreamUnr double2 per thread, every load of
+    // a chunk issued before its stores (x may alias y / z)
+    const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
+    for (int64_t ci = blockIdx.x; ci < chunks; ci += gridDim.x) {
+        const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
+        double2 xv[kStreamUnr], yv[kStreamUnr], zv[kStreamUnr];
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u) {
+            const int64_t i = 2 * (p0 + u * kThreads);
+            if (OP == OP_SCAL || OP == OP_AXPBY || OP == OP_AXPY_DEV) xv[u] = ld2(x + i);
+            if (OP != OP_ZERO && OP != OP_SCAL) yv[u] = ld2(y + i);
+            if (OP == OP_SUB3) zv[u] = ld2(z + i);
         }
-        const int64_t i = 2 * p;
-        double2 r;
-        if (OP == OP_ZERO) r = make_double2(0.0, 0.0);
-        if (OP == OP_COPY) r = ld2(y + i);
-        if (OP == OP_SCAL) {
-            r = ld2(x + i);
-            r.x *= a;
-            r.y *= a;
+#pragma unroll
+        for (int u = 0; u < kStreamUnr; ++u) {
+            double2 r = make_double2(0.0, 0.0);
+            if (OP == OP_COPY) r = yv[u];
+            if (OP == OP_SCAL) r = make_double2(xv[u].x * a, xv[u].y * a);
+            if (OP == OP_AXPBY)  // nek axpby: x(i) = x(i)*alpha + y(i)*beta (nek_vectors.f90:250-256)
+                r = make_double2(xv[u].x * a + yv[u].x * b, xv[u].y * a + yv[u].y * b);
+            if (OP == OP_SUB3) r = make_double2(yv[u].x - zv[u].x, yv[u].y - zv[u].y);
+            if (OP == OP_AXPY_DEV) r = make_double2(fma(a, yv[u].x, xv[u].x), fma(a, yv[u].y, xv[u].y));
+            st2(x + 2 * (p0 + u * kThreads), r);
         }
-        if (OP == OP_AXPBY) {  // nek axpby: x(i) = x(i)*alpha + y(i)*beta (nek_vectors.f90:250-256)
-            const double2 xv = ld2(x + i), yv = ld2(y + i);
-            r.x = xv.x * a + yv.x * b;
-            r.y = xv.y * a + yv.y * b;
-        }
-        if (OP == OP_SUB3) {
-            const double2 yv = ld2(y + i), zv = ld2(z + i);
-            r.x = yv.x - zv.x;
-            r.y = yv.y - zv.y;
-        }
-        if (OP == OP_AXPY_DEV) {
-            const double2 xv = ld2(x + i), yv = ld2(y + i);
-            r.x = fma(a, yv.x, xv.x);
-            r.y = fma(a, yv.y, xv.y);
-        }
-        st2(x + i, r);
+    }
+    if (do_time && blockIdx.x == 0 && threadIdx.x == 0) {  // scalar time component
+        const int64_t i = time_off;
+        if (OP == OP_ZERO) x[i] = 0.0;
+        if (OP == OP_COPY) x[i] = y[i];
+        if (OP == OP_SCAL) x[i] = x[i] * a;
+        if (OP == OP_AXPBY) x[i] = x[i] * a + y[i] * b;
+        if (OP == OP_SUB3) x[i] = y[i] - z[i];
+        if (OP == OP_AXPY_DEV) x[i] = fma(a, y[i], x[i]);
     }
 }
 
