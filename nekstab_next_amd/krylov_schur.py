@@ -20,6 +20,7 @@ The dense k x k work runs on the host (lapack.py), identically on every rank.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -172,3 +173,75 @@ def ritz_vector(ctx: NekContext, Q: Basis, vecs: np.ndarray, i: int, out_re: Nek
     out_re.scal(beta)
     out_im.scal(beta)
     return a_r, a_i
+
+
+def orthonormality_report(ctx: NekContext, Q: Basis, k: int) -> np.ndarray:
+    """Gram matrix G[i, j] = <q_i, q_j>_W (k_dot, no time term) of Q[0:k] — the self-check the
+    reference writes to ``orthonormality.dat`` after the solve (eigensolvers.f90:335-345).  One
+    multi-dot per column over the columns after it (upper triangle, k(k+1)/2 dots in k launches)."""
+    G = np.zeros((k, k))
+    h = ctx.h1
+    for i in range(k):
+        n = k - i
+        ctx.call("nkv_block_dot", ctx.w.data_ptr(), Q.col_ptr(i), n, Q.col_ptr(i), h[:n].data_ptr(), ctx.ws.data_ptr(),
+                 0, ctx.stream)
+        ctx.comm.allreduce_(h[:n])
+        row = h[:n].cpu().numpy()
+        G[i, i:] = row
+        G[i:, i] = row
+    ctx.check_nan()
+    return G
+
+
+def outpost_ks(ctx: NekContext, res: KrylovSchurResult, outdir: str, evop: str = "d", period: float = 1.0,
+               maxmodes: int = 20, session: str = "nek", k: int | None = None,
+               orthonormality: bool = True) -> dict:
+    """The end of the in-tree ``krylov_schur`` (eigensolvers.f90:335-349) and ``outpost_ks``
+    (:472-640): ``orthonormality.dat``; ``Spectre_H<evop>.dat`` (re, im, residual of every Ritz
+    value, 3E15.7) and ``Spectre_NS<evop>.dat`` (log-transformed, divided by the sampling period
+    dt*nsteps); for the first ``converged`` modes, up to ``maxmodes``: the eigenmode
+    Q(:,1:k) vecs(:,i), normalised so ||Re||^2 + ||Im||^2 = 1, written as ``<evop>Re`` /
+    ``<evop>Im`` field files numbered 1.. (time = output number), and its log-transformed value
+    appended to ``Spectre_NS<evop>_conv.dat`` (2E15.7).  The reference skips modes whose
+    gradient norm exceeds 1.1 (Nek5000 ``norm_grad``, a spectral-element derivative): that filter
+    needs the mesh and is not applied here.  Returns the written mode indices."""
+    from . import fld
+    from .checkpoint import log_transform
+
+    k = res.vecs.shape[0] if k is None else k
+    lay = ctx.layout
+    os.makedirs(outdir, exist_ok=True)
+    if orthonormality:
+        G = orthonormality_report(ctx, res.Q, k)
+        if ctx.comm.rank == 0:
+            with open(os.path.join(outdir, "orthonormality.dat"), "w") as fh:
+                for i in range(k):
+                    fh.write(f"Norm of the {i + 1:4d}th mode = {np.sqrt(G[i, i]):20.14f}\n")
+                    for j in range(i + 1, k):
+                        fh.write(f"Orthogonality between mode {i + 1:4d} and mode {j + 1:4d} = {G[i, j]:15.7E}\n")
+                    fh.write("\n")
+    if ctx.comm.rank == 0:
+        with open(os.path.join(outdir, f"Spectre_H{evop}.dat"), "w") as f1, \
+                open(os.path.join(outdir, f"Spectre_NS{evop}.dat"), "w") as f2:
+            for v, r in zip(res.vals[:k], res.residual[:k]):
+                f1.write(f"{v.real:15.7E}{v.imag:15.7E}{r:15.7E}\n")
+                lt = log_transform(v)
+                f2.write(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}{r:15.7E}\n")
+    written = []
+    re_v, im_v = ctx.vector(), ctx.vector()
+    conv_lines = []
+    for i in range(res.converged):
+        if len(written) >= maxmodes:
+            break
+        ritz_vector(ctx, res.Q, res.vecs, i, re_v, im_v, k=k)
+        num = len(written) + 1
+        for vec, name in ((re_v, f"{evop}Re"), (im_v, f"{evop}Im")):
+            f = fld.fld_from_vector(lay, vec.to_packed(), time=float(num), istep=num)
+            fld.write_fld(os.path.join(outdir, fld.fld_name(name, session, lay.rank, num)), f)
+        lt = log_transform(res.vals[i])
+        conv_lines.append(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}\n")
+        written.append(i)
+    if ctx.comm.rank == 0:
+        with open(os.path.join(outdir, f"Spectre_NS{evop}_conv.dat"), "w") as fh:
+            fh.writelines(conv_lines)
+    return dict(modes=written)

@@ -40,3 +40,37 @@ def test_restart_from_checkpoint_matches_uninterrupted(gpu, tmp_path):
     conv = ref.residual < 1e-6
     np.testing.assert_allclose(res.vals[conv], ref.vals[conv], rtol=1e-12)
     np.testing.assert_allclose(np.sort(res.vals[conv].real)[::-1], exact, atol=1e-9)
+
+
+def test_outpost_ks_files(gpu, tmp_path):
+    """End of the in-tree solver: orthonormality.dat, Spectre_H/NS(_conv) files and the Re/Im
+    eigenmode field files (eigensolvers.f90:335-349, 472-640)."""
+    from nekstab_next_amd import fld
+    from nekstab_next_amd.krylov_schur import outpost_ks
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=32)
+    d, exact = syn.diag_spectrum(lay)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    k = 16
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=k, schur_tgt=5))
+    out = outpost_ks(ctx, res, str(tmp_path), evop="d", period=2.0, maxmodes=4)
+    assert out["modes"] == list(range(min(4, res.converged)))
+    lines = open(tmp_path / "orthonormality.dat").read().split("\n")
+    norms = [float(l.split("=")[1]) for l in lines if l.startswith("Norm of")]
+    orth = [float(l.split("=")[1]) for l in lines if l.startswith("Orthogonality")]
+    assert len(norms) == k and len(orth) == k * (k - 1) // 2
+    assert max(abs(n - 1.0) for n in norms) < 1e-12 and max(abs(o) for o in orth) < 1e-12
+    sh = np.loadtxt(tmp_path / "Spectre_Hd.dat")
+    sn = np.loadtxt(tmp_path / "Spectre_NSd.dat")
+    assert sh.shape == (k, 3) and sn.shape == (k, 3)
+    np.testing.assert_allclose(sh[:, 0], res.vals.real, rtol=1e-6)
+    np.testing.assert_allclose(sn[:, 0], np.log(np.abs(res.vals)) / 2.0, rtol=1e-6, atol=1e-7)
+    conv = np.atleast_2d(np.loadtxt(tmp_path / "Spectre_NSd_conv.dat"))
+    assert conv.shape == (len(out["modes"]), 2)
+    for num in range(1, len(out["modes"]) + 1):
+        re = ctx.vector().from_packed(fld.vector_from_fld(lay, fld.read_fld(str(tmp_path / fld.fld_name("dRe", "nek", 0, num)))))
+        im = ctx.vector().from_packed(fld.vector_from_fld(lay, fld.read_fld(str(tmp_path / fld.fld_name("dIm", "nek", 0, num)))))
+        assert abs(ctx.dot(re, re, False) + ctx.dot(im, im, False) - 1.0) < 1e-10

@@ -98,8 +98,10 @@ def run(names, E, rounds, js, only=None):
     jmax = max(js)
     dev = torch.device("cuda", 0)
     Lc = lay.c_struct()
+    ldpad = int(os.environ.get("NKV_TUNE_LDPAD", "0"))   # extra doubles of column stride (multiple of 4096)
+    Lc.ld += ldpad
     Lp = ctypes.byref(Lc)
-    Q = torch.empty((jmax + 1, lay.ld), dtype=torch.float64, device=dev)
+    Q = torch.empty((jmax + 1, Lc.ld), dtype=torch.float64, device=dev)
     lib0 = libs[names[0]]
     st = torch.cuda.current_stream().cuda_stream
     for i in range(jmax + 1):
