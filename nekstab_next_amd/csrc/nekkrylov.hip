@@ -66,6 +66,9 @@ namespace {
 #ifndef NKV_DC_FIELDLOOP
 #define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
 #endif
+#ifndef NKV_D2_MAXB
+#define NKV_D2_MAXB NKV_MAXB  // workgroups of the two-vector multi-dot
+#endif
 #ifndef NKV_D2_FIELDLOOP
 #define NKV_D2_FIELDLOOP 1  // two-vector multi-dot: one block walks all weighted fields of a tile
 #endif
@@ -1519,7 +1522,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     // large problems: one block row walks every field of its tiles (weights read once per tile)
     const int nf = (large && NKV_D2_FIELDLOOP) ? L->n_wf : 1;
     const int gy = L->n_wf / nf;
-    int bx = kMaxBlocks / gy;
+    int bx = (NKV_D2_MAXB < kMaxBlocks ? NKV_D2_MAXB : kMaxBlocks) / gy;
     if (bx > tpf) bx = tpf;
     if (bx < 1) bx = 1;
     const int B = bx * gy;
