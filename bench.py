@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-restart", action="store_true", help="skip the restart-rotation measurement")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="at one GPU, route every partial through a world-1 RCCL group (collective cost)")
     args = ap.parse_args()
 
     import torch
@@ -161,7 +163,7 @@ def main():
     from nekstab_next_amd.profiling import PhaseTimer
     from nekstab_next_amd.vector import NekContext
 
-    comm = init_from_env(os.environ.get("NKV_BACKEND", "nccl"))
+    comm = init_from_env(os.environ.get("NKV_BACKEND", "nccl"), force_collectives=args.force_collectives)
     rank, world = comm.rank, comm.world
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)

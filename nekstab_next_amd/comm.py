@@ -17,8 +17,11 @@ import torch.distributed as dist
 class Comm:
     """One process per GPU.  ``world == 1`` makes every collective a no-op."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_collectives: bool = False):
         self.group = group
+        # force_collectives: issue the all-reduces even at world size 1 (an initialised world-1
+        # group) — measures the collective path's cost without peers (bench.py --force-collectives)
+        self.force = bool(force_collectives) and dist.is_available() and dist.is_initialized()
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
@@ -33,7 +36,7 @@ class Comm:
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place SUM all-reduce of a device partial (deterministic: RCCL gives every rank the
         same bits, so host LAPACK stays replicated on identical data)."""
-        if self.world > 1:
+        if self.world > 1 or self.force:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 
@@ -42,16 +45,32 @@ class Comm:
             dist.barrier(group=self.group)
 
     def max_scalar(self, x: float, device=None) -> float:
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
 
-def init_from_env(backend: str | None = None) -> Comm:
-    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*) if present."""
+def init_from_env(backend: str | None = None, force_collectives: bool = False) -> Comm:
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*) if present.
+    ``force_collectives`` at world size 1: initialise a world-1 group anyway and route every
+    partial through it (the cost of the collective path without peers)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and force_collectives and not dist.is_initialized():
+        import socket
+
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(0)
+            kw["device_id"] = torch.device("cuda", 0)
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **kw)
+        return Comm(force_collectives=True)
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"

@@ -86,3 +86,54 @@ def test_two_ranks_match_one_rank(gpu):
             sel = sorted(set(sel))
             assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) < 1e-12
         np.testing.assert_array_equal(out[(2, 0)][key][4], out[(2, 1)][key][4])  # identical H on ranks
+
+
+_RCCL_SCRIPT = r'''
+import os, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch, torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1,
+                        device_id=torch.device("cuda", 0))
+from nekstab_next_amd import synthetic as syn
+from nekstab_next_amd.comm import Comm
+from nekstab_next_amd.config import KrylovSchurConfig
+from nekstab_next_amd.krylov_schur import krylov_schur
+from nekstab_next_amd.layout import box3d_layout
+from nekstab_next_amd.operators import DiagOperator
+from nekstab_next_amd.vector import NekContext
+out = {}
+for forced in (False, True):
+    comm = Comm(force_collectives=forced)   # forced: world 1, every partial through RCCL all_reduce
+    assert comm.backend == "nccl"
+    lay = box3d_layout(96)
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=comm, max_cols=48)
+    d, _ = syn.laplacian_shift_invert(lay)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    for mode in ("dcgs2", "cgs2"):
+        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4, mode=mode))
+        out[(forced, mode)] = (r.vals, r.H, r.mstart_history)
+    assert comm.max_scalar(3.0, device=ctx.device) == 3.0
+for mode in ("dcgs2", "cgs2"):
+    a, b = out[(False, mode)], out[(True, mode)]
+    np.testing.assert_array_equal(a[0], b[0]); np.testing.assert_array_equal(a[1], b[1]); assert a[2] == b[2]
+dist.destroy_process_group()
+print("RCCL path ok")
+'''
+
+
+def test_rccl_collective_path_single_gpu(gpu, tmp_path):
+    """The nccl (= RCCL) backend on the real device: a world-1 process group with the collective
+    code path forced on, so every partial dot goes through dist.all_reduce on the compute stream
+    between the HIP kernels (the 8-GPU path minus the peers).  Results must be bit-identical to
+    the no-collective run.  Runs in a child process so the test process holds no process group."""
+    import subprocess
+
+    script = tmp_path / "rccl_path.py"
+    script.write_text(_RCCL_SCRIPT)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, str(script), ROOT, str(_free_port())], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "RCCL path ok" in p.stdout
