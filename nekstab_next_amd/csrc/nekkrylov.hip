@@ -730,14 +730,15 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
         af[k].x = fma(-yc, qbv.x, af[k].x);
         af[k].y = fma(-yc, qbv.y, af[k].y);
-#if NKV_DC_EXPERIMENT == 1   // timing experiment only: skip the stores (wrong results)
-        if (af[k].x == 12345.678) {
+        // NKV_DC_EXPERIMENT (timing only, wrong results): 1 skips both stores, 2 skips the q_j store
+#if NKV_DC_EXPERIMENT >= 1
+        if (af[k].x == 12345.678)
 #endif
         st2s(qj + r0 + k * 2 * kThreads, qbv);
-        st2s(f + r0 + k * 2 * kThreads, af[k]);
 #if NKV_DC_EXPERIMENT == 1
-        }
+        if (af[k].x == 12345.678)
 #endif
+        st2s(f + r0 + k * 2 * kThreads, af[k]);
     }
 }
 

@@ -58,6 +58,7 @@ VARIANTS = {
     "unr1_ntst0": {"NKV_NT_ST": 0, "NKV_STREAM_UNR": 1},
     "unr8": {"NKV_STREAM_UNR": 8},
     "dc_nostore": {"NKV_DC_EXPERIMENT": 1},
+    "dc_noqstore": {"NKV_DC_EXPERIMENT": 2},
     "d2_b768": {"NKV_D2_MAXB": 768},
     "d2_b512": {"NKV_D2_MAXB": 512},
     "d2_b256": {"NKV_D2_MAXB": 256},
