@@ -1,0 +1,28 @@
+"""bench.py's byte models (CPU): the executed-bytes model of each mode against the SURVEY.md §8(d)
+4-pass CGS2 model, and the kernel-family bookkeeping the roofline line relies on."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_byte_models_order():
+    N, N_w, n_v, m = 100_014_464, 90_472_448, 22_618_112, 128
+    survey = bench.survey_model_bytes(N, N_w, n_v, m)
+    cgs2u = bench.executed_bytes(N, N_w, n_v, m, "cgs2-unfused")
+    cgs2 = bench.executed_bytes(N, N_w, n_v, m, "cgs2")
+    dcgs2 = bench.executed_bytes(N, N_w, n_v, m, "dcgs2")
+    assert dcgs2 < cgs2 < cgs2u <= survey * 1.001
+    # 4 -> 3 -> 2 reads of the basis per step (the basis dominates at m = 128)
+    assert 0.70 < cgs2 / cgs2u < 0.80
+    assert 0.62 < dcgs2 / cgs2 < 0.72
+
+
+def test_survey_model_matches_worked_total():
+    # config 3, m=128 -> sum_j B(j) = 26.03 TB (+ 3N per step for the matvec)
+    N, N_w, n_v, m = 100_014_464, 90_472_448, 22_618_112, 128
+    tot = bench.survey_model_bytes(N, N_w, n_v, m) - m * 8.0 * 3 * N
+    assert abs(tot / 1e12 - 26.03) < 0.01
