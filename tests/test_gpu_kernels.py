@@ -398,6 +398,20 @@ def test_empty_shard(gpu):
     assert ctx.scal[4].item() == 0.0 and not np.any(ctx.h2[:4].cpu().numpy())
     V = torch.eye(4, dtype=torch.float64, device=ctx.device).flatten()
     ctx.call("nkv_rotate", Q.ptr, 4, V.data_ptr(), 4, ctx.stream)
+    ctx.call("nkv_rotate_cols", Q.ptr, 4, V.data_ptr(), 4, 2, ctx.stream)
+    # DCGS2 entry points: zero partials from the empty shard, the time slot still follows the update
+    from nekstab_next_amd._lib import NKV_X_IS_LAST
+    hd = ctx.hd[:8]
+    ctx.call("nkv_block_dot2", ctx.w.data_ptr(), Q.ptr, 4, Q.col_ptr(3), f.ptr, hd.data_ptr(), ctx.ws.data_ptr(),
+             NKV_X_IS_LAST, ctx.stream)
+    assert not np.any(hd.cpu().numpy())
+    coef = np.zeros(3 * 3 + 8)
+    coef[2 * 3 + 1] = coef[2 * 3 + 4] = 1.0
+    ctx.coef[: coef.size].copy_(torch.as_tensor(coef))
+    t0 = Q[3].time
+    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, 3, ctx.coef.data_ptr(), Q.col_ptr(3), f.ptr, Q.col_ptr(4),
+             ctx.scal[5:6].data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+    assert ctx.scal[5].item() == 0.0 and Q[3].time == t0
     torch.cuda.synchronize()
 
 
