@@ -150,19 +150,19 @@ def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVect
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
     m = j - 1
-    h, coef, nrm = ctx.hd[: 2 * j], ctx.coef, ctx.scal[3:4]
+    h, nrm = ctx.hd[: 2 * j], ctx.scal[3:4]
+    hp, cp, np_ = h.data_ptr(), ctx.coef.data_ptr(), nrm.data_ptr()   # raw pointers: few host objects per step
     u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot2")
-    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, h.data_ptr(), ws, tf | NKV_X_IS_LAST, st)
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, hp, ws, tf | NKV_X_IS_LAST, st)
     if tm:
         tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), h[j:].data_ptr(), None if first else nrm.data_ptr(),
-                Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(), ws, st)
+    ctx.call_nl("nkv_dcgs2_coef", m, hp, hp + 8 * j, None if first else np_, Hd.t.data_ptr(), Hd.k + 1, cp, ws, st)
     if tm:
         tm.begin("dcgs2_update")
-    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, coef.data_ptr(), u, f.ptr, Q.col_ptr(j), nrm.data_ptr(), ws,
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, u, f.ptr, Q.col_ptr(j), np_, ws,
              NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
     if tm:
         tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N + lay.n_v))

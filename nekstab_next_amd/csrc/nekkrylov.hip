@@ -285,10 +285,13 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
 }
 
 // Second stage: out[c] = sum_b partials[c][b] in a fixed order (+ replicated time term).
+// Columns c >= jc are a second right-hand side (two-vector multi-dot): their time term uses tb2
+// and basis column c - jc.
 __global__ __launch_bounds__(kThreads) void k_reduce_cols(const double* __restrict__ partials, int B,
                                                           double* __restrict__ out,
                                                           const double* __restrict__ ta, int64_t lda,
                                                           const double* __restrict__ tb,
+                                                          const double* __restrict__ tb2, int jc,
                                                           int* __restrict__ nan_flag) {
     __shared__ double lds4[4];
     const int c = blockIdx.x;
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_cols(const double* __restri
     for (int b = threadIdx.x; b < B; b += kThreads) s += partials[(int64_t)c * B + b];
     s = block_sum(s, lds4);
     if (threadIdx.x == 0) {
-        if (ta) s += ta[(int64_t)c * lda] * tb[0];
+        if (ta) s += (c < jc) ? ta[(int64_t)c * lda] * tb[0] : ta[(int64_t)(c - jc) * lda] * tb2[0];
         if (s != s) atomicOr(nan_flag, 1);
         out[c] = s;
     }
@@ -1237,7 +1240,7 @@ int launch_block_dot_p(const nkv_layout* L, const double* w, const double* Q, in
     const int64_t T = rows_of(L);
     const bool tdot = (flags & NKV_TIME) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, out,
-                       tdot ? Q + T : nullptr, ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+                       tdot ? Q + T : nullptr, ld, tdot ? f + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -1426,7 +1429,7 @@ int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int 
         // ||f||^2 time term: (uparam(1)==2.1 / real_dot) only on the rank owning the replicated scalar
         const bool tdot = (flags & NKV_TIME) && L->rank0;
         hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev,
-                           tdot ? f + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nan_flag_of(ws));
+                           tdot ? f + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
         NKV_LAUNCHED();
     }
     return NKV_OK;
@@ -1498,7 +1501,7 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     NKV_LAUNCHED();
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, B, hout_dev, tdot ? Q + T : nullptr,
-                       L->ld, tdot ? f + T : nullptr, nan_flag_of(ws));
+                       L->ld, tdot ? f + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -1540,11 +1543,9 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     }
     const int64_t T = rows_of(L);
     const bool tdot = (flags & NKV_TIME) && L->rank0;
-    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, h_dev,
-                       tdot ? Q + T : nullptr, L->ld, tdot ? x + T : nullptr, nan_flag_of(ws));
-    NKV_LAUNCHED();
-    hipLaunchKernelGGL(k_reduce_cols, dim3(j), dim3(kThreads), 0, st, part + (int64_t)j * B, tpf > 0 ? B : 0,
-                       h_dev + j, tdot ? Q + T : nullptr, L->ld, tdot ? y + T : nullptr, nan_flag_of(ws));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2 * j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, h_dev,
+                       tdot ? Q + T : nullptr, L->ld, tdot ? x + T : nullptr, tdot ? y + T : nullptr, j,
+                       nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -1595,7 +1596,7 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     NKV_LAUNCHED();
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev, tdot ? fout + T : nullptr,
-                       (int64_t)0, tdot ? fout + T : nullptr, nan_flag_of(ws));
+                       (int64_t)0, tdot ? fout + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }

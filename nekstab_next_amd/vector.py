@@ -219,10 +219,12 @@ class Basis:
         self.ctx = ctx
         self.k = k
         self.storage = torch.zeros((k, ctx.layout.ld), dtype=torch.float64, device=ctx.device)
+        self._ptr = self.storage.data_ptr()          # the allocation never moves
+        self._stride = ctx.layout.ld * 8
 
     @property
     def ptr(self) -> int:
-        return self.storage.data_ptr()
+        return self._ptr
 
     def __len__(self) -> int:
         return self.k
@@ -233,7 +235,9 @@ class Basis:
         return NekVector(self.ctx, self.storage[i])
 
     def col_ptr(self, i: int) -> int:
-        return self.storage[i].data_ptr()
+        if not 0 <= i < self.k:
+            raise IndexError(i)
+        return self._ptr + i * self._stride
 
 
 # ---------------------------------------------------------------------------------------------
