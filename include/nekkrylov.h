@@ -177,6 +177,12 @@ int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y
                 void* stream);
 int nkv_op_rot2(const nkv_layout* L, const double* c, const double* s, const double* d_rest,
                 const double* x, double* y, int transpose, void* stream);
+/* op_cdiag: complex diagonal y = c x (conj: conj(c) x) on a re/im pair vector (the complex
+ * cmplx_nek_vector{re, im} of nek_vectors.f90:33-42 stored as one real vector: in every segment the
+ * re half first, then the im half; c = cr + i ci read at the re rows); y.time = 0.  The synthetic
+ * resolvent (i omega - L)^-1 of resolvent_analysis (linear_stab.f90:120-163). */
+int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const double* x, double* y, int conj,
+                 void* stream);
 
 /* ---- shard-independent synthetic data ----------------------------------------------------
  * x[row] = 2*u - 1, u = hash(seed, field, global point) in [0,1) with 53 exact bits, for live

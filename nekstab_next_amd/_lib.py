@@ -80,6 +80,7 @@ _SIGNATURES = {
     "nkv_rotate_cols": (c_int, [_L, _P, c_int, _P, c_int, c_int, _P]),
     "nkv_op_diag": (c_int, [_L, _P, _P, _P, c_double, _P]),
     "nkv_op_rot2": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
+    "nkv_op_cdiag": (c_int, [_L, _P, _P, _P, _P, c_int, _P]),
     "nkv_fill_hash": (c_int, [_L, _P, c_uint64, c_int64, c_int64, _P]),
 }
 

@@ -1162,6 +1162,27 @@ __global__ __launch_bounds__(kThreads) void k_op_rot2(const double* __restrict__
     if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = 0.0;
 }
 
+// Complex diagonal operator on a re/im pair vector (nekstab_next_amd.layout.PairLayout): in each
+// segment (weighted field f: rows [f sv, f sv + n_v); pressure: [n_wf sv, n_wf sv + n_p)) the first
+// half holds re, the second im.  y = c x (conj: y = conj(c) x), c = cr + i ci read at the re rows.
+// grid (bx, n_wf + 1): blockIdx.y = segment (n_wf = pressure).
+__global__ __launch_bounds__(kThreads) void k_op_cdiag(const double* __restrict__ cr,
+                                                       const double* __restrict__ ci,
+                                                       const double* __restrict__ x, double* __restrict__ y,
+                                                       int64_t sv, int64_t n_v, int64_t n_p, int n_wf,
+                                                       int64_t time_off, double sg) {
+    const int seg = blockIdx.y;
+    const int64_t base = (int64_t)seg * sv;
+    const int64_t half = (seg < n_wf ? n_v : n_p) / 2;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < half; i += (int64_t)gridDim.x * kThreads) {
+        const int64_t r = base + i, m = r + half;
+        const double a = cr[r], b = sg * ci[r], xr = x[r], xi = x[m];
+        y[r] = a * xr - b * xi;
+        y[m] = b * xr + a * xi;
+    }
+    if (seg == 0 && blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = 0.0;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1769,6 +1790,23 @@ int nkv_op_rot2(const nkv_layout* L, const double* c, const double* s, const dou
     const int64_t rows = rows_of(L);
     hipLaunchKernelGGL(k_op_rot2, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), c, s, d_rest, x,
                        y, L->sv, rows, rows, transpose ? -1.0 : 1.0);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const double* x, double* y, int conj,
+                 void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(cr, "cr"));
+    CHECK(check_ptr(ci, "ci"));
+    CHECK(check_ptr(x, "x"));
+    CHECK(check_ptr(y, "y"));
+    if (x == y) return fail(NKV_EINVAL, "cdiag cannot run in place");
+    if ((L->n_v % 2) || (L->n_p % 2)) return fail(NKV_ESHAPE, "cdiag: not a re/im pair layout (odd n_v / n_p)");
+    const int64_t half = (L->n_v > L->n_p ? L->n_v : L->n_p) / 2;
+    int bx = grid_for(half, 1024);
+    hipLaunchKernelGGL(k_op_cdiag, dim3(bx, L->n_wf + 1), dim3(kThreads), 0, S(stream), cr, ci, x, y, L->sv, L->n_v,
+                       L->n_p, L->n_wf, rows_of(L), conj ? -1.0 : 1.0);
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -9,8 +9,10 @@ core/linear_stab.f90:12-119, 295-383).
 
 The operator is any :class:`~nekstab_next_amd.operators.LinearOperator` (the exponential
 propagator of a Nek5000 run in production; synthetic operators in the tests) with the sampling
-time ``t`` (``exponential_prop%t``).  ``resolvent_analysis`` (complex vectors through an inner GMRES
-on Id - A^T) is not provided: its operator is a Nek5000 time integration.
+time ``t`` (``exponential_prop%t``).
+* :func:`resolvent_analysis` — svds of a resolvent operator on complex (re/im pair) vectors,
+  sigma <- sigma**2, ``Spectrum_Sr.dat``.  The resolvent's body (forced Nek5000 run + inner GMRES
+  on Id - A^T) is the caller's operator.
 """
 from __future__ import annotations
 
@@ -84,3 +86,35 @@ def transient_growth_analysis(ctx: NekContext, A: LinearOperator, seed: NekVecto
             get_vec(v, V, r.vvecs[:, i], k_dim)
             _export(ctx, v, outdir, "pV", session, i + 1, float(i + 1))
     return dict(gain=gain, sigma=r.sigma, residuals=r.residuals, info=r.info, U=U, V=V, svd=r)
+
+
+def resolvent_analysis(ctx: NekContext, R: LinearOperator, seed: NekVector, k_dim: int = 100, nev: int = 2,
+                       tolerance: float = 1e-6, outdir: str | None = None, evop: str = "r") -> dict:
+    """``resolvent_analysis`` (core/linear_stab.f90:120-163): svds of the resolvent operator on
+    complex vectors, sigma <- sigma**2, ``Spectrum_S<evop>.dat`` (sigma^2, residual; 2E15.7).
+
+    ``ctx`` is a context on a :class:`~nekstab_next_amd.layout.PairLayout` (complex vectors as
+    re/im pair vectors, so the cmplx dot re.re + im.im is the layout's weighted dot and svds runs
+    unchanged); ``R`` maps complex to complex (``matvec``) with its adjoint (``rmatvec``).  In
+    nekStab R's body is a forced Nek5000 integration plus an inner GMRES
+    (linear_operators.f90:348-431) — any operator with that interface plugs in;
+    :class:`~nekstab_next_amd.operators.ComplexDiagOperator` is the synthetic, exactly known one.
+    The reference seeds re and im separately (prepare_seed on U%re, U%im, :147-148); here the
+    seed pair is normalised as one vector (the bidiagonalisation only needs its direction).  The
+    cmplx dot is real, so x and i x are independent directions and every singular value of the
+    complex operator appears twice in ``sigma2`` — as with LightKrylov's svds on
+    cmplx_nek_vector."""
+    from .layout import PairLayout
+
+    if not isinstance(ctx.layout, PairLayout):
+        raise ValueError("resolvent_analysis needs a NekContext on a PairLayout (complex vectors)")
+    U, V = ctx.basis(k_dim + 1), ctx.basis(k_dim + 1)
+    prepare_seed(seed, V[0])
+    r = svds(ctx, R, U, V, nev=nev, tolerance=tolerance)
+    gain = r.sigma ** 2   # sigma = sigma**2 (:157)
+    if outdir and ctx.comm.rank == 0:
+        os.makedirs(outdir, exist_ok=True)
+        with open(os.path.join(outdir, f"Spectrum_S{evop}.dat"), "w") as fh:
+            for s, res in zip(gain, r.residuals):
+                fh.write(f"{s:15.7E}{res:15.7E}\n")
+    return dict(sigma2=gain, residuals=r.residuals, info=r.info, U=U, V=V, svd=r)

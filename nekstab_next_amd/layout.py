@@ -159,3 +159,58 @@ def cylinder_layout(nelgv: int = 1996) -> NekLayout:
 def box3d_layout(nelgv: int, n_scalars: int = 1) -> NekLayout:
     """3-D lx1=8 layout with one scalar, as SURVEY.md §8(d) config 3 (E=44,176 -> N=1.0e8)."""
     return NekLayout(ldim=3, lx1=8, lx2=6, nelgv=nelgv, n_scalars=n_scalars)
+
+
+@dataclass(frozen=True)
+class PairLayout(NekLayout):
+    """A complex state vector ``cmplx_nek_vector{re, im}`` (core/nek_vectors.f90:33-42) stored as
+    ONE real vector: in every field segment (and the pressure segment) of this rank's shard the
+    ``re`` part of the base shard's elements comes first, then the ``im`` part.  The weighted dot
+    of two such vectors is re.re + im.im — the cmplx dot (:164-175) — so every kernel, the
+    Gram–Schmidt and the solvers run on complex vectors unchanged.  Rank r owns the pair of the
+    base layout's element block: elem_range = 2 x base elem_range, for any world size."""
+
+    base_nelgv: int = 0
+
+    def elem_range(self, rank: int | None = None) -> tuple[int, int]:
+        r = self.rank if rank is None else rank
+        return 2 * ((r * self.base_nelgv) // self.world), 2 * (((r + 1) * self.base_nelgv) // self.world)
+
+    def shard(self, rank: int, world: int) -> "PairLayout":
+        return pair_layout(NekLayout(self.ldim, self.lx1, self.lx2, self.base_nelgv, self.n_scalars, self.ifpo,
+                                     rank, world))
+
+    @property
+    def base(self) -> NekLayout:
+        return NekLayout(self.ldim, self.lx1, self.lx2, self.base_nelgv, self.n_scalars, self.ifpo, self.rank,
+                         self.world)
+
+    def pack(self, re, im):
+        """Host: padded pair vector from two padded base vectors (time: re's)."""
+        import numpy as np
+
+        b = self.base
+        out = np.zeros(self.ld)
+        for (_, s0, n0), (_, s1, _) in zip(b.field_slices(), self.field_slices()):
+            out[s1: s1 + n0] = re[s0: s0 + n0]
+            out[s1 + n0: s1 + 2 * n0] = im[s0: s0 + n0]
+        out[self.time_offset] = re[b.time_offset]
+        return out
+
+    def unpack(self, v):
+        """Host: (re, im) padded base vectors from a pair vector."""
+        import numpy as np
+
+        b = self.base
+        re, im = np.zeros(b.ld), np.zeros(b.ld)
+        for (_, s0, n0), (_, s1, _) in zip(b.field_slices(), self.field_slices()):
+            re[s0: s0 + n0] = v[s1: s1 + n0]
+            im[s0: s0 + n0] = v[s1 + n0: s1 + 2 * n0]
+        re[b.time_offset] = v[self.time_offset]
+        return re, im
+
+
+def pair_layout(lay: NekLayout) -> PairLayout:
+    """The complex (re/im pair) counterpart of ``lay`` (same shard)."""
+    return PairLayout(lay.ldim, lay.lx1, lay.lx2, 2 * lay.nelgv, lay.n_scalars, lay.ifpo, lay.rank, lay.world,
+                      base_nelgv=lay.nelgv)

@@ -135,3 +135,28 @@ class CallableOperator(LinearOperator):
         if self._rmv is None:
             raise NotImplementedError("operator has no adjoint")
         self._rmv(x, y)
+
+
+class ComplexDiagOperator(LinearOperator):
+    """y = C x, C complex diagonal, on complex vectors stored as re/im pair vectors
+    (:class:`~nekstab_next_amd.layout.PairLayout`); ``rmatvec`` applies conj(C) — the adjoint under
+    the cmplx dot re.re + im.im.  ``cr``/``ci`` are padded pair-layout vectors read at the re rows
+    (:func:`~nekstab_next_amd.synthetic.resolvent_diag`).  The synthetic stand-in for nekStab's
+    ``resolvent_op`` (core/linear_operators.f90:309-431), whose body is a forced Nek5000 run."""
+
+    def __init__(self, ctx: NekContext, cr, ci):
+        from .layout import PairLayout
+
+        if not isinstance(ctx.layout, PairLayout):
+            raise ValueError("ComplexDiagOperator needs a NekContext on a PairLayout")
+        self.ctx = ctx
+        self.cr = cr if isinstance(cr, torch.Tensor) else _dev(ctx, cr)
+        self.ci = ci if isinstance(ci, torch.Tensor) else _dev(ctx, ci)
+        if self.cr.numel() != ctx.layout.ld or self.ci.numel() != ctx.layout.ld:
+            raise ValueError("cr, ci must have layout.ld entries")
+
+    def matvec(self, x: NekVector, y: NekVector) -> None:
+        self.ctx.call("nkv_op_cdiag", self.cr.data_ptr(), self.ci.data_ptr(), x.ptr, y.ptr, 0, self.ctx.stream)
+
+    def rmatvec(self, x: NekVector, y: NekVector) -> None:
+        self.ctx.call("nkv_op_cdiag", self.cr.data_ptr(), self.ci.data_ptr(), x.ptr, y.ptr, 1, self.ctx.stream)

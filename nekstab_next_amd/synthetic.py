@@ -203,3 +203,35 @@ def laplacian_shift_invert(lay: NekLayout, seed: int = 3, k0: int = 3, frac: flo
     mu = 1.0 / (lam(ks) - sigma)
     exact = mu[np.argsort(-np.abs(mu), kind="stable")][:n_exact]
     return d, exact
+
+
+# ---- resolvent (complex) test operator ----------------------------------------------------------
+
+RESOLVENT_GAMMAS = (0.02, 0.05, 0.11, 0.2, 0.31)   # decay rates of the least-stable modes
+
+
+def resolvent_diag(lay, omega: float = 0.3, gammas=RESOLVENT_GAMMAS, seed: int = 3):
+    """Resolvent R = (i omega I - L)^-1 of a W-normal stable diagonal L, on the re/im pair layout
+    ``lay`` (a :class:`~nekstab_next_amd.layout.PairLayout` shard): eigenvalues of L are
+    -gamma_p (seeded weighted dofs, ``gammas``) and a bulk -g in [0.5, 5] over the global weighted
+    dofs; pressure -1.  Returns (cr, ci) padded pair vectors (R's diagonal at the re rows) and the
+    exact leading singular values 1/sqrt(omega^2 + gamma^2), decreasing."""
+    base = lay.base
+    n = base.n_wf * base.pts_v * base.nelgv
+    pos = _dominant_positions(base, len(gammas), seed)
+    cr = np.zeros(lay.ld)
+    ci = np.zeros(lay.ld)
+    for (_, s0, n0), (_, s1, _), f in zip(base.field_slices(), lay.field_slices(), range(base.n_wf + 1)):
+        if f < base.n_wf:
+            g = weighted_global_index(base, f)
+            gam = 0.5 + 4.5 * g / n
+            for p, gm in zip(pos, gammas):
+                gam[g == p] = gm
+        else:
+            gam = np.ones(n0)
+        # 1/(i omega + gamma) = (gamma - i omega)/(gamma^2 + omega^2)
+        den = gam * gam + omega * omega
+        cr[s1: s1 + n0] = gam / den
+        ci[s1: s1 + n0] = -omega / den
+    sv = np.sort(1.0 / np.sqrt(omega * omega + np.asarray(gammas) ** 2))[::-1]
+    return cr, ci, sv
