@@ -18,8 +18,26 @@ their quirks:
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 from scipy.linalg import lapack as _lp
+
+_tp = None
+
+
+def _one_thread():
+    """Single-threaded BLAS for the k x k problems: deterministic bits on every rank (the restart
+    decisions are taken redundantly per rank and must agree), and no thread fan-out for tiny work."""
+    global _tp
+    if _tp is None:
+        try:
+            from threadpoolctl import ThreadpoolController
+
+            _tp = ThreadpoolController()
+        except Exception:  # noqa: BLE001  (threadpoolctl missing: run as configured)
+            _tp = False
+    return _tp.limit(limits=1, user_api="blas") if _tp else contextlib.nullcontext()
 
 
 def eig(A: np.ndarray):
@@ -27,7 +45,8 @@ def eig(A: np.ndarray):
     descending (lapack_wrapper.f90:114-177).  Returns (vals[n] complex, vecs[n,n] complex)."""
     A = np.array(A, dtype=np.float64, order="F", copy=True)
     n = A.shape[0]
-    wr, wi, _vl, vr, info = _lp.dgeev(A, compute_vl=0, compute_vr=1, lwork=max(1, 4 * n))
+    with _one_thread():
+        wr, wi, _vl, vr, info = _lp.dgeev(A, compute_vl=0, compute_vr=1, lwork=max(1, 4 * n))
     if info != 0:
         raise np.linalg.LinAlgError(f"dgeev info={info}")
     vals = wr + 1j * wi
@@ -65,8 +84,9 @@ def schur(A: np.ndarray):
     Returns (T, Z, vals) with vals in Schur-diagonal order."""
     A = np.array(A, dtype=np.float64, order="F", copy=True)
     n = A.shape[0]
-    t, _sdim, wr, wi, vs, _work, info = _lp.dgees(lambda a, b: int(select_eigvals(a, b)), A, compute_v=1,
-                                                  sort_t=1, lwork=max(1, 3 * n))
+    with _one_thread():
+        t, _sdim, wr, wi, vs, _work, info = _lp.dgees(lambda a, b: int(select_eigvals(a, b)), A, compute_v=1,
+                                                      sort_t=1, lwork=max(1, 3 * n))
     if info not in (0, n + 1, n + 2):  # the reference ignores info; only hard failures raise here
         raise np.linalg.LinAlgError(f"dgees info={info}")
     return np.asfortranarray(t), np.asfortranarray(vs), wr + 1j * wi
@@ -75,8 +95,9 @@ def schur(A: np.ndarray):
 def ordschur(T: np.ndarray, Z: np.ndarray, selected: np.ndarray):
     """dtrsen(job='N', compq='V') moving ``selected`` to the leading block (:59-111)."""
     n = T.shape[0]
-    ts, qs, _wr, _wi, m, _s, _sep, info = _lp.dtrsen(np.asarray(selected, dtype=np.int32), T, Z, job="N",
-                                                     wantq=1, lwork=max(1, n), liwork=1)
+    with _one_thread():
+        ts, qs, _wr, _wi, m, _s, _sep, info = _lp.dtrsen(np.asarray(selected, dtype=np.int32), T, Z, job="N",
+                                                         wantq=1, lwork=max(1, n), liwork=1)
     if info != 0:
         raise np.linalg.LinAlgError(f"dtrsen info={info}")
     return np.asfortranarray(ts), np.asfortranarray(qs), int(m)
@@ -86,7 +107,9 @@ def lstsq(A: np.ndarray, b: np.ndarray) -> np.ndarray:
     """min ||A x - b||_2 via dgels('N'), lwork=2mn; x = b_tilde(1:n) (:248-300)."""
     A = np.array(A, dtype=np.float64, order="F", copy=True)
     m, n = A.shape
-    _lqr, x, info = _lp.dgels(A, np.array(b, dtype=np.float64, copy=True), trans="N", lwork=max(1, 2 * m * n))
+    with _one_thread():
+        _lqr, x, info = _lp.dgels(A, np.array(b, dtype=np.float64, copy=True), trans="N",
+                                  lwork=max(1, 2 * m * n))
     if info != 0:
         raise np.linalg.LinAlgError(f"dgels info={info}")
     return np.asarray(x[:n], dtype=np.float64)
