@@ -1,0 +1,141 @@
+/*
+ * arnoldi_c.c — a plain-C host driving the drop-in C ABI (include/nekkrylov.h) with no Python:
+ * the shape of what a Fortran bind(C) host does on each MPI rank.
+ *
+ *   build:  make -C examples/c_host   (gcc, the HIP runtime API and libnekkrylov.so)
+ *
+ *   run:    examples/c_host/arnoldi_c [E] [m]
+ *
+ * 3-D lx1=8 layout with one scalar (E elements), diagonal synthetic operator, seed from
+ * nkv_fill_hash, m DCGS2 Arnoldi steps (single rank: the all-reduces of INTEGRATION.md §2b are the
+ * identity), the closing re-orthogonalisation, then checks of W-orthonormality of the basis and of
+ * the Arnoldi relation A Q_m = Q_{m+1} H through the same ABI.  Exit status 0 on success.
+ */
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "nekkrylov.h"
+
+#define CK(x)                                                                             \
+    do {                                                                                  \
+        int rc_ = (x);                                                                    \
+        if (rc_ != NKV_OK) {                                                              \
+            fprintf(stderr, "%s failed (%d): %s\n", #x, rc_, nkv_last_error());          \
+            return 1;                                                                     \
+        }                                                                                 \
+    } while (0)
+#define HK(x)                                                                             \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                       \
+            return 1;                                                                     \
+        }                                                                                 \
+    } while (0)
+
+static int64_t roundup(int64_t n, int64_t m) { return (n + m - 1) / m * m; }
+
+int main(int argc, char** argv) {
+    const int E = argc > 1 ? atoi(argv[1]) : 512;
+    const int m = argc > 2 ? atoi(argv[2]) : 24;
+    const int ldim = 3, lx1 = 8, lx2 = 6, nsc = 1;
+    nkv_layout L;
+    L.n_v = (int64_t)lx1 * lx1 * lx1 * E;
+    L.n_p = (int64_t)lx2 * lx2 * lx2 * E;
+    L.n_wf = ldim + nsc;
+    L.sv = roundup(L.n_v, NKV_TILE);
+    L.sp = roundup(L.n_p, NKV_TILE);
+    L.ld = roundup((int64_t)L.n_wf * L.sv + L.sp + 1, NKV_TILE);
+    L.rank0 = 1;
+    const int64_t rows = (int64_t)L.n_wf * L.sv + L.sp;
+
+    if (nkv_abi_version() != NKV_ABI_VERSION) {
+        fprintf(stderr, "ABI mismatch\n");
+        return 1;
+    }
+    hipStream_t st;
+    HK(hipStreamCreate(&st));
+    double *Q, *f, *w, *d, *Hd, *hd, *coef, *nrm, *hcol, *ws;
+    const size_t vbytes = (size_t)L.ld * sizeof(double);
+    HK(hipMalloc((void**)&Q, (size_t)(m + 1) * vbytes));
+    HK(hipMalloc((void**)&f, vbytes));
+    HK(hipMalloc((void**)&d, vbytes));
+    HK(hipMalloc((void**)&w, (size_t)L.sv * sizeof(double)));
+    HK(hipMalloc((void**)&Hd, (size_t)m * (m + 1) * sizeof(double)));
+    HK(hipMalloc((void**)&hd, (size_t)2 * (m + 1) * sizeof(double)));
+    HK(hipMalloc((void**)&coef, (size_t)(3 * m + 8) * sizeof(double)));
+    HK(hipMalloc((void**)&nrm, 8 * sizeof(double)));
+    HK(hipMalloc((void**)&hcol, (size_t)(m + 2) * sizeof(double)));
+    const size_t wsb = nkv_workspace_bytes(&L, m + 1);
+    HK(hipMalloc((void**)&ws, wsb));
+    HK(hipMemsetAsync(ws, 0, wsb, st));
+    HK(hipMemsetAsync(Q, 0, (size_t)(m + 1) * vbytes, st));
+    HK(hipMemsetAsync(Hd, 0, (size_t)m * (m + 1) * sizeof(double), st));
+
+    /* weights: 1 on live points, 0 in the padding; operator: d_i in (0.05, 1) from the hash */
+    double* hw = (double*)calloc((size_t)L.sv, sizeof(double));
+    for (int64_t i = 0; i < L.n_v; ++i) hw[i] = 1.0;
+    HK(hipMemcpyAsync(w, hw, (size_t)L.sv * sizeof(double), hipMemcpyHostToDevice, st));
+    CK(nkv_fill_hash(&L, d, 99, 0, 0, st));
+    double* hdg = (double*)malloc(vbytes);
+    HK(hipMemcpyAsync(hdg, d, vbytes, hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < L.ld; ++i) hdg[i] = 0.525 + 0.475 * hdg[i];   /* [-1,1] -> [0.05, 1] */
+    HK(hipMemcpyAsync(d, hdg, vbytes, hipMemcpyHostToDevice, st));
+
+    /* q_1 = seed / ||seed||_W */
+    CK(nkv_fill_hash(&L, Q, 11, 0, 0, st));
+    CK(nkv_dot(&L, w, Q, Q, nrm, ws, 0, st));
+    CK(nkv_normalize_dev(&L, Q, nrm, NULL, 0, st));
+
+    /* m DCGS2 steps (a multi-rank host all-reduces hd and nrm in between) */
+    for (int j = 1; j <= m; ++j) {
+        double* u = Q + (int64_t)(j - 1) * L.ld;
+        CK(nkv_op_diag(&L, d, u, f, 0.0, st));
+        CK(nkv_block_dot2(&L, w, Q, j, u, f, hd, ws, NKV_X_IS_LAST, st));
+        CK(nkv_dcgs2_coef(j - 1, hd, hd + j, j == 1 ? NULL : nrm, Hd, m + 1, coef, ws, st));
+        CK(nkv_dcgs2_update(&L, w, Q, j - 1, coef, u, f, Q + (int64_t)j * L.ld, nrm, ws, NKV_TIME, st));
+    }
+    double* um = Q + (int64_t)m * L.ld;
+    CK(nkv_block_dot(&L, w, Q, m + 1, um, hd, ws, 0, st));
+    CK(nkv_dcgs2_coef(m, hd, NULL, nrm, Hd, m + 1, coef, ws, st));
+    CK(nkv_block_update(&L, w, Q, m, hd, um, NULL, ws, NKV_TIME, st));
+    CK(nkv_normalize_dev(&L, um, coef + 2 * m + 3, NULL, 0, st));
+    CK(nkv_check_status(ws, st));
+
+    double* H = (double*)malloc((size_t)m * (m + 1) * sizeof(double));
+    HK(hipMemcpyAsync(H, Hd, (size_t)m * (m + 1) * sizeof(double), hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+
+    /* checks through the ABI: G = Q^T W Q (column by column), and ||A q_c - Q H(:,c)||_W */
+    double orth = 0.0, arn = 0.0, hmax = 0.0;
+    double* g = (double*)malloc((size_t)(m + 1) * sizeof(double));
+    for (int c = 0; c <= m; ++c) {
+        CK(nkv_block_dot(&L, w, Q, m + 1, Q + (int64_t)c * L.ld, hd, ws, 0, st));
+        HK(hipMemcpyAsync(g, hd, (size_t)(m + 1) * sizeof(double), hipMemcpyDeviceToHost, st));
+        HK(hipStreamSynchronize(st));
+        for (int r = 0; r <= m; ++r) {
+            const double e = fabs(g[r] - (r == c ? 1.0 : 0.0));
+            if (e > orth) orth = e;
+        }
+    }
+    for (int i = 0; i < m * (m + 1); ++i) hmax = fmax(hmax, fabs(H[i]));
+    for (int c = 0; c < m; c += (m > 4 ? m / 4 : 1)) {
+        CK(nkv_op_diag(&L, d, Q + (int64_t)c * L.ld, f, 0.0, st));
+        HK(hipMemcpyAsync(hcol, H + (int64_t)c * (m + 1), (size_t)(c + 2) * sizeof(double), hipMemcpyHostToDevice, st));
+        CK(nkv_block_update(&L, w, Q, c + 2, hcol, f, nrm, ws, NKV_NORM2, st));
+        double r2;
+        HK(hipMemcpyAsync(&r2, nrm, sizeof(double), hipMemcpyDeviceToHost, st));
+        HK(hipStreamSynchronize(st));
+        arn = fmax(arn, sqrt(fabs(r2)));
+    }
+    printf("arnoldi_c: N=%lld m=%d  max|Q^T W Q - I| = %.3e  max ||A q - Q h|| / max|H| = %.3e  H(m+1,m) = %.6e\n",
+           (long long)(L.n_wf * L.n_v + L.n_p), m, orth, arn / hmax, H[(int64_t)(m - 1) * (m + 1) + m]);
+    const int ok = orth < 1e-12 && arn / hmax < 1e-12;
+    printf(ok ? "arnoldi_c: OK\n" : "arnoldi_c: FAILED\n");
+    (void)rows;
+    return ok ? 0 : 1;
+}

@@ -595,3 +595,18 @@ def test_arnoldi_long_vs_oracle(gpu, mode):
     idx = [0, 1, 150, 299, 300]
     G = np.array([[ctx.dot(Q[a], Q[b], time=False) for b in idx] for a in idx])
     assert np.max(np.abs(G - np.eye(len(idx)))) < 1e-12
+
+
+def test_c_host_example_runs(gpu):
+    """examples/c_host/arnoldi_c: 24 DCGS2 Arnoldi steps driven from plain C through the ABI (the
+    integration a Fortran/C host performs), W-orthonormality and the Arnoldi relation to 1e-12."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "c_host", "arnoldi_c")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True, timeout=300)
+    p = subprocess.run([exe, "512", "24"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "arnoldi_c: OK" in p.stdout

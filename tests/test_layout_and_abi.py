@@ -114,3 +114,15 @@ def test_product_fails_loudly_without_gpu():
 
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         NekContext(NekLayout(ldim=2, lx1=4, lx2=2, nelgv=4))
+
+
+def test_c_host_example_builds():
+    """The plain-C host (examples/c_host: gcc + HIP runtime API + libnekkrylov.so, no Python)
+    compiles and links against the header and library as shipped."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run(["make", "-s", "-B", "-C", os.path.join(root, "examples", "c_host")], capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert os.path.exists(os.path.join(root, "examples", "c_host", "arnoldi_c"))
