@@ -1,0 +1,105 @@
+! arnoldi_f.f90 — a Fortran host (the reference's language) running DCGS2 Arnoldi through the C ABI:
+! the replacement of arnoldi_factorization / update_hessenberg_matrix (krylov_decomposition.f90)
+! by the loop of INTEGRATION.md §2b on one rank (gop = identity), then W-orthonormality and the
+! Arnoldi relation A Q_m = Q_{m+1} H checked through the same calls.   usage: arnoldi_f [E [m]]
+program arnoldi_f
+   use iso_c_binding
+   use nkv_bindings
+   implicit none
+   type(nkv_layout), target :: L
+   type(c_ptr) :: Q, f, d, w, Hdev, hv, coef, nrm, hcol, ws, st, u
+   integer :: E, m, j, c, r, nargs
+   character(len=32) :: arg
+   integer(c_size_t) :: vbytes, wsb
+   real(c_double), allocatable, target :: hw(:), H(:, :), g(:), dh(:)
+   real(c_double), target :: r2
+   real(c_double) :: orth, arn, hmax
+
+   E = 512; m = 24
+   nargs = command_argument_count()
+   if (nargs >= 1) then; call get_command_argument(1, arg); read (arg, *) E; end if
+   if (nargs >= 2) then; call get_command_argument(2, arg); read (arg, *) m; end if
+   st = c_null_ptr                              ! the null (default) stream
+
+   L%n_v = 512_c_int64_t*E; L%n_p = 216_c_int64_t*E; L%n_wf = 4; L%rank0 = 1    ! 3-D lx1=8, one scalar
+   L%sv = ((L%n_v + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
+   L%sp = ((L%n_p + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
+   L%ld = ((L%n_wf*L%sv + L%sp + 1 + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
+   if (nkv_abi_version() /= 1) stop 'ABI mismatch'
+
+   vbytes = int(L%ld, c_size_t)*8
+   call ck(hipMalloc(Q, (m + 1)*vbytes), 'hipMalloc Q')
+   call ck(hipMalloc(f, vbytes), 'hipMalloc f')
+   call ck(hipMalloc(d, vbytes), 'hipMalloc d')
+   call ck(hipMalloc(w, int(L%sv, c_size_t)*8), 'hipMalloc w')
+   call ck(hipMalloc(Hdev, int(m*(m + 1), c_size_t)*8), 'hipMalloc H')
+   call ck(hipMalloc(hv, int(2*(m + 1), c_size_t)*8), 'hipMalloc h')
+   call ck(hipMalloc(coef, int(3*m + 8, c_size_t)*8), 'hipMalloc coef')
+   call ck(hipMalloc(nrm, 64_c_size_t), 'hipMalloc nrm')
+   call ck(hipMalloc(hcol, int(m + 2, c_size_t)*8), 'hipMalloc hcol')
+   wsb = nkv_workspace_bytes(L, m + 1)
+   call ck(hipMalloc(ws, wsb), 'hipMalloc ws')
+   call ck(hipMemset(ws, 0, wsb), 'memset ws')
+   call ck(hipMemset(Q, 0, (m + 1)*vbytes), 'memset Q')
+   call ck(hipMemset(Hdev, 0, int(m*(m + 1), c_size_t)*8), 'memset H')
+
+   allocate (hw(L%sv), dh(L%ld), H(m + 1, m), g(m + 1))
+   hw = 0.0d0; hw(1:L%n_v) = 1.0d0                          ! bm1s: 1 on live points
+   call ck(hipMemcpy(w, c_loc(hw), int(L%sv, c_size_t)*8, hipMemcpyHostToDevice), 'w')
+   call ck(nkv_fill_hash(L, d, 99_c_int64_t, 0_c_int64_t, 0_c_int64_t, st), 'hash d')
+   call ck(hipMemcpy(c_loc(dh), d, vbytes, hipMemcpyDeviceToHost), 'd down')
+   dh = 0.525d0 + 0.475d0*dh                                 ! diag in (0.05, 1)
+   call ck(hipMemcpy(d, c_loc(dh), vbytes, hipMemcpyHostToDevice), 'd up')
+
+   call ck(nkv_fill_hash(L, Q, 11_c_int64_t, 0_c_int64_t, 0_c_int64_t, st), 'seed')
+   call ck(nkv_dot(L, w, Q, Q, nrm, ws, 0, st), 'seed norm')
+   call ck(nkv_normalize_dev(L, Q, nrm, c_null_ptr, 0, st), 'normalise')
+
+   do j = 1, m
+      u = col(Q, j - 1, L%ld)
+      call ck(nkv_op_diag(L, d, u, f, 0.0d0, st), 'matvec')
+      call ck(nkv_block_dot2(L, w, Q, j, u, f, hv, ws, NKV_X_IS_LAST, st), 'block_dot2')
+      if (j == 1) then
+         call ck(nkv_dcgs2_coef(j - 1, hv, off(hv, j), c_null_ptr, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'coef')
+      else
+         call ck(nkv_dcgs2_coef(j - 1, hv, off(hv, j), nrm, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'coef')
+      end if
+      call ck(nkv_dcgs2_update(L, w, Q, j - 1, coef, u, f, col(Q, j, L%ld), nrm, ws, NKV_TIME, st), 'update')
+   end do
+   u = col(Q, m, L%ld)
+   call ck(nkv_block_dot(L, w, Q, m + 1, u, hv, ws, 0, st), 'close dot')
+   call ck(nkv_dcgs2_coef(m, hv, c_null_ptr, nrm, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'close coef')
+   call ck(nkv_block_update(L, w, Q, m, hv, u, c_null_ptr, ws, NKV_TIME, st), 'close update')
+   call ck(nkv_normalize_dev(L, u, off(coef, 2*m + 3), c_null_ptr, 0, st), 'close normalise')
+   call ck(nkv_check_status(ws, st), 'NaN check')
+   call ck(hipMemcpy(c_loc(H), Hdev, int(m*(m + 1), c_size_t)*8, hipMemcpyDeviceToHost), 'H down')
+
+   orth = 0.0d0
+   do c = 0, m
+      call ck(nkv_block_dot(L, w, Q, m + 1, col(Q, c, L%ld), hv, ws, 0, st), 'gram')
+      call ck(hipMemcpy(c_loc(g), hv, int(m + 1, c_size_t)*8, hipMemcpyDeviceToHost), 'g down')
+      do r = 0, m
+         if (r == c) then
+            orth = max(orth, abs(g(r + 1) - 1.0d0))
+         else
+            orth = max(orth, abs(g(r + 1)))
+         end if
+      end do
+   end do
+   hmax = maxval(abs(H)); arn = 0.0d0
+   do c = 0, m - 1, max(1, m/4)
+      call ck(nkv_op_diag(L, d, col(Q, c, L%ld), f, 0.0d0, st), 'matvec')
+      call ck(hipMemcpy(hcol, c_loc(H(1, c + 1)), int(c + 2, c_size_t)*8, hipMemcpyHostToDevice), 'hcol')
+      call ck(nkv_block_update(L, w, Q, c + 2, hcol, f, nrm, ws, NKV_NORM2, st), 'residual')
+      call ck(hipMemcpy(c_loc(r2), nrm, 8_c_size_t, hipMemcpyDeviceToHost), 'r2')
+      arn = max(arn, sqrt(abs(r2)))
+   end do
+   print '(a,i0,a,i0,a,es10.3,a,es10.3,a,es14.6)', 'arnoldi_f: N=', L%n_wf*L%n_v + L%n_p, ' m=', m, &
+      '  max|Q^T W Q - I| = ', orth, '  max||A q - Q h||/max|H| = ', arn/hmax, '  H(m+1,m) = ', H(m + 1, m)
+   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12) then
+      print '(a)', 'arnoldi_f: OK'
+   else
+      print '(a)', 'arnoldi_f: FAILED'
+      stop 1
+   end if
+end program arnoldi_f

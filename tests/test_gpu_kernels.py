@@ -610,3 +610,18 @@ def test_c_host_example_runs(gpu):
     p = subprocess.run([exe, "512", "24"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "arnoldi_c: OK" in p.stdout
+
+
+def test_fortran_host_example_runs(gpu):
+    """examples/fortran_host/arnoldi_f: the DCGS2 loop of INTEGRATION.md §2b from Fortran through the
+    bind(C) interface (the reference's language): W-orthonormality and Arnoldi relation to 1e-12."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "fortran_host", "arnoldi_f")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True, timeout=300)
+    p = subprocess.run([exe, "512", "24"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "arnoldi_f: OK" in p.stdout

@@ -126,3 +126,15 @@ def test_c_host_example_builds():
                        text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert os.path.exists(os.path.join(root, "examples", "c_host", "arnoldi_c"))
+
+
+def test_fortran_host_example_builds():
+    """The Fortran host (examples/fortran_host: the bind(C) module of INTEGRATION.md §2 compiled
+    with amdflang, linked to libnekkrylov.so) builds against the header's ABI as shipped."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run(["make", "-s", "-B", "-C", os.path.join(root, "examples", "fortran_host")],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert os.path.exists(os.path.join(root, "examples", "fortran_host", "arnoldi_f"))
