@@ -65,7 +65,7 @@ def executed_bytes(N, N_w, n_v, m, mode):
         elif mode == "cgs2-unfused":
             tot += 2 * dot + upd + (upd + 8.0 * n_v)
         elif mode == "dcgs2":   # two-vector dot over j-1 streamed columns (+ u, A u); dual update over j-1
-            tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v) + 8.0 * ((j - 1) * N + 4 * N + n_v)
+            tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v) + 8.0 * ((j - 1) * N + 4 * N)
         else:
             raise ValueError(mode)
         tot += (0.0 if mode == "dcgs2" else 8.0 * 2 * N) + 8.0 * 3 * N   # normalise pass (not in dcgs2) + matvec

@@ -91,17 +91,18 @@ int main(int argc, char** argv) {
     CK(nkv_dot(&L, w, Q, Q, nrm, ws, 0, st));
     CK(nkv_normalize_dev(&L, Q, nrm, NULL, 0, st));
 
-    /* m DCGS2 steps (a multi-rank host all-reduces hd and nrm in between) */
+    /* m DCGS2 steps (a multi-rank host all-reduces hd after block_dot2:
+       beta^2 of the provisional column is the dot's own entry hd[j-1]) */
     for (int j = 1; j <= m; ++j) {
         double* u = Q + (int64_t)(j - 1) * L.ld;
         CK(nkv_op_diag(&L, d, u, f, 0.0, st));
         CK(nkv_block_dot2(&L, w, Q, j, u, f, hd, ws, NKV_X_IS_LAST, st));
-        CK(nkv_dcgs2_coef(j - 1, hd, hd + j, j == 1 ? NULL : nrm, Hd, m + 1, coef, ws, st));
-        CK(nkv_dcgs2_update(&L, w, Q, j - 1, coef, u, f, Q + (int64_t)j * L.ld, nrm, ws, NKV_TIME, st));
+        CK(nkv_dcgs2_coef(j - 1, hd, hd + j, j == 1 ? NULL : hd + (j - 1), Hd, m + 1, coef, ws, st));
+        CK(nkv_dcgs2_update(&L, w, Q, j - 1, coef, u, f, Q + (int64_t)j * L.ld, NULL, ws, NKV_TIME, st));
     }
     double* um = Q + (int64_t)m * L.ld;
     CK(nkv_block_dot(&L, w, Q, m + 1, um, hd, ws, 0, st));
-    CK(nkv_dcgs2_coef(m, hd, NULL, nrm, Hd, m + 1, coef, ws, st));
+    CK(nkv_dcgs2_coef(m, hd, NULL, hd + m, Hd, m + 1, coef, ws, st));
     CK(nkv_block_update(&L, w, Q, m, hd, um, NULL, ws, NKV_TIME, st));
     CK(nkv_normalize_dev(&L, um, coef + 2 * m + 3, NULL, 0, st));
     CK(nkv_check_status(ws, st));

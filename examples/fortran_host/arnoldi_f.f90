@@ -62,13 +62,13 @@ program arnoldi_f
       if (j == 1) then
          call ck(nkv_dcgs2_coef(j - 1, hv, off(hv, j), c_null_ptr, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'coef')
       else
-         call ck(nkv_dcgs2_coef(j - 1, hv, off(hv, j), nrm, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'coef')
+         call ck(nkv_dcgs2_coef(j - 1, hv, off(hv, j), off(hv, j - 1), Hdev, int(m + 1, c_int64_t), coef, ws, st), 'coef')
       end if
-      call ck(nkv_dcgs2_update(L, w, Q, j - 1, coef, u, f, col(Q, j, L%ld), nrm, ws, NKV_TIME, st), 'update')
+      call ck(nkv_dcgs2_update(L, w, Q, j - 1, coef, u, f, col(Q, j, L%ld), c_null_ptr, ws, NKV_TIME, st), 'update')
    end do
    u = col(Q, m, L%ld)
    call ck(nkv_block_dot(L, w, Q, m + 1, u, hv, ws, 0, st), 'close dot')
-   call ck(nkv_dcgs2_coef(m, hv, c_null_ptr, nrm, Hdev, int(m + 1, c_int64_t), coef, ws, st), 'close coef')
+   call ck(nkv_dcgs2_coef(m, hv, c_null_ptr, off(hv, m), Hdev, int(m + 1, c_int64_t), coef, ws, st), 'close coef')
    call ck(nkv_block_update(L, w, Q, m, hv, u, c_null_ptr, ws, NKV_TIME, st), 'close update')
    call ck(nkv_normalize_dev(L, u, off(coef, 2*m + 3), c_null_ptr, 0, st), 'close normalise')
    call ck(nkv_check_status(ws, st), 'NaN check')

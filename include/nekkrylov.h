@@ -135,17 +135,19 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
                        unsigned flags, void* stream);
 
 /* ---- DCGS2: classical Gram–Schmidt with delayed re-orthogonalisation (two reads of Q per step,
- * two all-reduces, no separate normalisation pass).  Same replacement target as the CGS2 entry
- * points above (update_hessenberg_matrix, krylov_decomposition.f90:103-189); the
+ * ONE all-reduce per step, no separate normalisation pass).  Same replacement target as the CGS2
+ * entry points above (update_hessenberg_matrix, krylov_decomposition.f90:103-189); the
  * re-orthogonalisation AND the normalisation of q_j are folded into step j+1, the previous H
- * column corrected on the device.  Step j (m = j-1 final columns; Q column m holds u = beta q_j,
- * beta^2 in nrm (NULL at the first step: u is normalised); f = A u):
+ * column corrected on the device.  Step j (m = j-1 final columns; Q column m holds u = beta q_j;
+ * f = A u):
  *   nkv_block_dot2(Q, j, x=u, y=f) -> h[0:j] = Q^T W u, h[j:2j] = Q^T W f          (all-reduce 2j)
  *   nkv_dcgs2_coef(m, h, h+j, nrm, H, ldh, coef)   H(m,m-1) = beta, row m corrected, column m = c;
  *                                                  coef = [x | c | rinv, y, (beta r)^2, s | a]
- *   nkv_dcgs2_update(Q, m, coef, u, f, Q col j, nrm) -> column m final, column j = the next u,
- *                                                  nrm = ||next u||_W^2              (all-reduce 1)
- * After the last step (m = mend): nkv_block_dot(Q, m+1, u), nkv_dcgs2_coef(m, h, NULL, nrm, ...),
+ *   nkv_dcgs2_update(Q, m, coef, u, f, Q col j, NULL) -> column m final, column j = the next u
+ * nrm points at beta^2: h + m (= u^T W u, the dot's last entry) -- or NULL at the first step
+ * (u normalised, beta = 1), or a separately reduced ||u||_W^2 (nkv_dcgs2_update with a non-NULL
+ * nrm2 computes it, fused, from the f it writes: one more all-reduce per step).
+ * After the last step (m = mend): nkv_block_dot(Q, m+1, u) -> h, nkv_dcgs2_coef(m, h, NULL, h+m, ...),
  * nkv_block_update(Q, m, h, u), nkv_normalize_dev(u, coef+2m+3).
  * H is column-major with leading dimension ldh (>= m+1) in device memory. */
 int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j, const double* x,

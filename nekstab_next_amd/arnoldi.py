@@ -143,15 +143,15 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
 
 def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool) -> None:
     """Step j (1-based) of DCGS2 Arnoldi: Q[0:j-1] final, Q[j-1] = u = beta q_j provisional and not
-    yet normalised (beta^2 in ctx.scal[3], unless ``first``: then u is normalised), f = A u.  On
-    return Q[j-1] is final, Q[j] = the next u (its norm^2 in ctx.scal[3]), H columns 0..j-2 final
-    and column j-1 provisional, H(j, j-1) pending."""
+    yet normalised (unless ``first``: then u is normalised), f = A u.  On return Q[j-1] is final,
+    Q[j] = the next u, H columns 0..j-2 final and column j-1 provisional, H(j, j-1) pending.
+    beta^2 = u^T W u is the last entry of the step's own Q^T W u, so one all-reduce per step."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
     m = j - 1
-    h, nrm = ctx.hd[: 2 * j], ctx.scal[3:4]
-    hp, cp, np_ = h.data_ptr(), ctx.coef.data_ptr(), nrm.data_ptr()   # raw pointers: few host objects per step
+    h = ctx.hd[: 2 * j]
+    hp, cp = h.data_ptr(), ctx.coef.data_ptr()   # raw pointers: few host objects per step
     u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot2")
@@ -159,14 +159,13 @@ def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVect
     if tm:
         tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, hp, hp + 8 * j, None if first else np_, Hd.t.data_ptr(), Hd.k + 1, cp, ws, st)
+    ctx.call_nl("nkv_dcgs2_coef", m, hp, hp + 8 * j, None if first else hp + 8 * m, Hd.t.data_ptr(), Hd.k + 1, cp,
+                ws, st)
     if tm:
         tm.begin("dcgs2_update")
-    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, u, f.ptr, Q.col_ptr(j), np_, ws,
-             NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, u, f.ptr, Q.col_ptr(j), None, ws, NKV_TIME, st)
     if tm:
-        tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N + lay.n_v))
-    ctx.comm.allreduce_(nrm)
+        tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N))
 
 
 def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
@@ -175,7 +174,7 @@ def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
-    h, coef, nrm = ctx.hd[: m + 1], ctx.coef, ctx.scal[3:4]
+    h, coef = ctx.hd[: m + 1], ctx.coef
     u = Q.col_ptr(m)
     if tm:
         tm.begin("block_dot")
@@ -183,8 +182,8 @@ def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
     if tm:
         tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, nrm.data_ptr(), Hd.t.data_ptr(), Hd.k + 1, coef.data_ptr(),
-                ws, st)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, h.data_ptr() + 8 * m, Hd.t.data_ptr(), Hd.k + 1,
+                coef.data_ptr(), ws, st)
     if tm:
         tm.begin("block_update")
     ctx.call("nkv_block_update", w, Q.ptr, m, h.data_ptr(), u, None, ws, NKV_TIME, st)

@@ -745,7 +745,9 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
     }
 }
 
-template <int kPairs>
+// kNrm = false: no ||f||_W^2 partial (the next step's dot of u with itself supplies beta^2, see
+// nkv_dcgs2_coef), so the weights are not read and no partials are written.
+template <int kPairs, bool kNrm>
 __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
                                                            const double* __restrict__ coef,
                                                            double* __restrict__ qj, const double* __restrict__ win,
@@ -774,8 +776,13 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
             f[time_off] = win[time_off] * (sc * rinv) - s2 - qb * yc;
         }
     }
-    double nrm = 0.0;
     double2 af[kPairs];
+    if constexpr (!kNrm) {
+        for (int t = blockIdx.x; t < tiles_total; t += gridDim.x)
+            dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af);
+        return;
+    }
+    double nrm = 0.0;
 #if NKV_DC_FIELDLOOP
     // work unit = one row tile of EVERY weighted field (the norm's weights are read once per unit,
     // not once per field), then the pressure tiles one by one
@@ -1594,7 +1601,7 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     CHECK(check_ptr(fout, "fout"));
     CHECK(check_ptr(ws, "ws"));
     if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
-    if (!coef_dev || !nrm2_dev) return fail(NKV_EINVAL, "coef/nrm2 is NULL");
+    if (!coef_dev) return fail(NKV_EINVAL, "coef is NULL");
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
     const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
@@ -1608,13 +1615,12 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
-    if (large)
-        hipLaunchKernelGGL(k_dcgs2_update<NKV_DC_PAIRS>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
-                           win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else
-        hipLaunchKernelGGL(k_dcgs2_update<NKV_PAIRS_SMALL>, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
-                           win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
+    auto kern = large ? (nrm2_dev ? k_dcgs2_update<NKV_DC_PAIRS, true> : k_dcgs2_update<NKV_DC_PAIRS, false>)
+                      : (nrm2_dev ? k_dcgs2_update<NKV_PAIRS_SMALL, true> : k_dcgs2_update<NKV_PAIRS_SMALL, false>);
+    hipLaunchKernelGGL(kern, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj, win, fout, w, L->sv, tpf,
+                       tiles_w, tiles_total, T, dt, part);
     NKV_LAUNCHED();
+    if (!nrm2_dev) return NKV_OK;
     const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
     hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev, tdot ? fout + T : nullptr,
                        (int64_t)0, tdot ? fout + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));

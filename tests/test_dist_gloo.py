@@ -55,9 +55,10 @@ def _cgs2_arnoldi(lay, w, d, q0, m, comm):
 
 def _dcgs2_arnoldi(lay, w, d, q0, m, comm):
     """Sharded DCGS2 Arnoldi in numpy on one rank, the algebra of nkv_block_dot2 /
-    nkv_dcgs2_coef / nkv_dcgs2_update with deferred normalisation: ONE all-reduce of
-    [Q^T W u ; Q^T W A u] (2j values) and one of ||f||^2 per step; column j holds u = beta q_j until
-    step j+1 divides the raw dots by beta, corrects H and finalises it; a closing pass at the end."""
+    nkv_dcgs2_coef / nkv_dcgs2_update with deferred normalisation: ONE all-reduce per step, of
+    [Q^T W u ; Q^T W A u] (2j values); column j holds u = beta q_j until step j+1 takes
+    beta^2 = u^T W u from that dot, divides the raw dots by beta, corrects H and finalises it; a
+    closing pass at the end."""
     wf = np.zeros(lay.ld)
     for f in range(lay.n_wf):
         wf[f * lay.sv: f * lay.sv + lay.n_v] = w
@@ -84,6 +85,7 @@ def _dcgs2_arnoldi(lay, w, d, q0, m, comm):
         h = torch.as_tensor(np.concatenate([Q[:j] @ (wf * Q[mm]), Q[:j] @ (wf * f)]))
         comm.allreduce_(h)
         h = h.numpy()
+        beta = None if j == 1 else float(np.sqrt(h[mm]))
         a, r, row, Hold, s = correct(mm, h[:j], beta)
         b, bj = h[j: j + mm] * s, h[j + mm] * s * s
         t = row @ a
@@ -93,14 +95,12 @@ def _dcgs2_arnoldi(lay, w, d, q0, m, comm):
         qbar = (Q[mm] * s - a @ Q[:mm]) / r
         Q[mm] = qbar
         u = f * s / r - x @ Q[:mm] - qbar * y
-        nrm = torch.as_tensor([np.sum(wf * u * u)])
-        comm.allreduce_(nrm)
-        beta = float(np.sqrt(nrm.item()))
         H[:j, j - 1] = c
         Q[j] = u
     hq = torch.as_tensor(Q[: m + 1] @ (wf * Q[m]))
     comm.allreduce_(hq)
     hq = hq.numpy()
+    beta = float(np.sqrt(hq[m]))
     correct(m, hq, beta)
     r2s = hq[m] - (hq[:m] / beta) @ (hq[:m] / beta) * beta * beta
     Q[m] = (Q[m] - hq[:m] @ Q[:m]) / np.sqrt(r2s)

@@ -412,6 +412,9 @@ def test_empty_shard(gpu):
     ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, 3, ctx.coef.data_ptr(), Q.col_ptr(3), f.ptr, Q.col_ptr(4),
              ctx.scal[5:6].data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
     assert ctx.scal[5].item() == 0.0 and Q[3].time == t0
+    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, 3, ctx.coef.data_ptr(), Q.col_ptr(3), f.ptr, Q.col_ptr(4),
+             None, ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+    assert Q[3].time == t0
     torch.cuda.synchronize()
 
 
@@ -528,9 +531,10 @@ def test_dcgs2_coef_flags_breakdown(gpu):
         ctx.check_nan()
 
 
+@pytest.mark.parametrize("with_norm", [True, False])
 @pytest.mark.parametrize("name", list(DC_LAYOUTS))
 @pytest.mark.parametrize("m", [0, 1, 6, 31])
-def test_dcgs2_update_vs_numpy(gpu, name, m):
+def test_dcgs2_update_vs_numpy(gpu, name, m, with_norm):
     lay = DC_LAYOUTS[name]
     ctx, w = make_ctx(lay, max_cols=40)
     Q = ctx.basis(m + 2)
@@ -552,15 +556,19 @@ def test_dcgs2_update_vs_numpy(gpu, name, m):
     Qh = Q.storage.cpu().numpy()
     fh = f.to_packed()
     nrm = ctx.scal[3:4]
+    nrm.fill_(-1.0)
     ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, m, ctx.coef.data_ptr(), Q.col_ptr(m), f.ptr,
-             Q.col_ptr(m + 1), nrm.data_ptr(), ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+             Q.col_ptr(m + 1), nrm.data_ptr() if with_norm else None, ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
     qbar = (Qh[m] * sc - a @ Qh[:m]) * rinv          # every row incl. the time slot (NKV_TIME)
     fref = fh * sc * rinv - x @ Qh[:m] - qbar * yc
     np.testing.assert_allclose(Q.storage[m].cpu().numpy(), qbar, rtol=1e-12, atol=1e-13)
     np.testing.assert_allclose(Q.storage[m + 1].cpu().numpy(), fref, rtol=1e-12, atol=1e-13)
     np.testing.assert_array_equal(f.to_packed(), fh)   # the matvec output is only read
     wf = _wfull(lay, w)
-    np.testing.assert_allclose(nrm.item(), np.sum(wf * fref * fref), rtol=1e-12)
+    if with_norm:
+        np.testing.assert_allclose(nrm.item(), np.sum(wf * fref * fref), rtol=1e-12)
+    else:
+        assert nrm.item() == -1.0   # no norm requested: nothing reduced, nothing written
 
 
 @pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])

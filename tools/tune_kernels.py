@@ -149,6 +149,10 @@ def run(names, E, rounds, js, only=None):
                                                         Q[j - 1].data_ptr(), f.data_ptr(), f2.data_ptr(), nrm.data_ptr(),
                                                         ws.data_ptr(), 0x1, st),
                              8.0 * ((j - 1) * N + 4 * N + nv)),
+            "dcgs2_upd0": (lambda: L.nkv_dcgs2_update(Lp, w.data_ptr(), Q.data_ptr(), j - 1, coefs[j].data_ptr(),
+                                                      Q[j - 1].data_ptr(), f.data_ptr(), f2.data_ptr(), None,
+                                                      ws.data_ptr(), 0x1, st),
+                           8.0 * ((j - 1) * N + 4 * N)),
             "finish": (lambda: L.nkv_arnoldi_finish(Lp, f.data_ptr(), nrm1.data_ptr(), f2.data_ptr(), 0, None, None,
                                                     None, 0, st), 16.0 * N),
             "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
