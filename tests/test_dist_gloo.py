@@ -165,7 +165,7 @@ def test_sharded_cgs2_equals_unsharded():
     q0 = q0 / np.sqrt(np.sum(wf * q0 * q0))
     Href = _cgs2_arnoldi(g, w, d, q0, 12, Comm())
     assert np.max(np.abs(H0 - Href)) <= 1e-12 * np.max(np.abs(Href))
-    # DCGS2 (sharded, 2 all-reduces per step) builds the same Arnoldi factorisation as CGS2
+    # DCGS2 (sharded, 1 all-reduce per step) builds the same Arnoldi factorisation as CGS2
     assert np.max(np.abs(Hd0 - Href)) <= 1e-12 * np.max(np.abs(Href))
 
 

@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ks(world_rank_pair, out, port):
+def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400):
     rank, world = world_rank_pair
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -41,14 +41,14 @@ def _run_ks(world_rank_pair, out, port):
 
         res = {}
         comm = Comm()
-        lay = box3d_layout(96).shard(rank, world)
+        lay = box3d_layout(E_box).shard(rank, world)
         ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=comm, max_cols=48)
         d, _ = syn.laplacian_shift_invert(lay)
         seed = ctx.vector()
         seed.fill_hash(11)
         r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4))
         res["lap"] = (r.vals, r.residual, r.mstart_history, r.schur_cnt, r.H)
-        lay2 = cylinder_layout(400).shard(rank, world)
+        lay2 = cylinder_layout(E_cyl).shard(rank, world)
         ctx2 = NekContext(lay2, weights=syn.mass_weights(lay2), comm=comm, max_cols=48)
         c, s, dr, _ = syn.rot2_operator(lay2)
         seed2 = ctx2.vector()
@@ -61,16 +61,20 @@ def _run_ks(world_rank_pair, out, port):
             dist.destroy_process_group()
 
 
-def test_two_ranks_match_one_rank(gpu):
+@pytest.mark.parametrize("world,E_box,E_cyl", [(2, 96, 400), (3, 97, 401)])
+def test_ranks_match_one_rank(gpu, world, E_box, E_cyl):
+    """Krylov–Schur on `world` gloo ranks sharing the GPU (the sharded HIP path, one shard per
+    process) reproduces the one-rank run; (3, 97, 401) gives ragged shards (32/32/33 and
+    133/134/134 elements)."""
     mgr = mp.Manager()
     out = mgr.dict()
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_run_ks, args=((0, 1), out, _free_port()))
+    p = ctx.Process(target=_run_ks, args=((0, 1), out, _free_port(), E_box, E_cyl))
     p.start()
     p.join()
     assert p.exitcode == 0
     port = _free_port()
-    procs = [ctx.Process(target=_run_ks, args=((r, 2), out, port)) for r in range(2)]
+    procs = [ctx.Process(target=_run_ks, args=((r, world), out, port, E_box, E_cyl)) for r in range(world)]
     for q in procs:
         q.start()
     for q in procs:
@@ -78,14 +82,14 @@ def test_two_ranks_match_one_rank(gpu):
         assert q.exitcode == 0
     for key in ("lap", "rot"):
         v1, r1, m1, c1, H1 = out[(1, 0)][key]
-        for rank in range(2):
-            v2, r2, m2, c2, H2 = out[(2, rank)][key]
+        for rank in range(world):
+            v2, r2, m2, c2, H2 = out[(world, rank)][key]
             assert m2 == m1 and c2 == c1
             conv = r1 < 1e-6
             sel = np.nonzero(conv)[0].tolist() + list(range(8))
             sel = sorted(set(sel))
             assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) < 1e-12
-        np.testing.assert_array_equal(out[(2, 0)][key][4], out[(2, 1)][key][4])  # identical H on ranks
+            np.testing.assert_array_equal(out[(world, 0)][key][4], H2)  # identical H on every rank
 
 
 _RCCL_SCRIPT = r'''
