@@ -52,6 +52,10 @@ extern "C" {
 
 /* Rows per tile: fields are padded to a multiple of this many doubles. */
 #define NKV_TILE 4096
+/* Most basis columns one multi-dot (nkv_block_dot / nkv_block_dot2) takes: its per-column partials
+ * live in LDS (64 B per column for the two-vector dot).  The reference's k_dim defaults to 100
+ * (main.f90:9); GMRES on the cylinder uses 200 (1cyl.usr:14). */
+#define NKV_MAX_COLS 1024
 
 /* Status codes (every entry point). */
 #define NKV_OK 0

@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 
 NKV_TILE = 4096
+NKV_MAX_COLS = 1024   # most columns per multi-dot (include/nekkrylov.h)
 NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE = 0, 1, 2, 3, 4
 NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2

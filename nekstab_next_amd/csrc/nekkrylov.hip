@@ -1430,7 +1430,7 @@ int nkv_block_dot(const nkv_layout* L, const double* w, const double* Q, int j, 
     CHECK(check_ptr(f, "f"));
     CHECK(check_ptr(ws, "ws"));
     if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
-    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    if (j < 1 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 1..%d", j, NKV_MAX_COLS);
     return launch_block_dot(L, w, Q, L->ld, j, f, h_dev, ws, flags, S(stream));
 }
 
@@ -1471,7 +1471,7 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     CHECK(check_ptr(f, "f"));
     CHECK(check_ptr(ws, "ws"));
     if (!h_dev || !hout_dev) return fail(NKV_EINVAL, "h_dev/hout_dev is NULL");
-    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    if (j < 1 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 1..%d", j, NKV_MAX_COLS);
     const unsigned upd_flags = (flags & NKV_TIME) ? NKV_TIME : 0u;
     const unsigned dot_flags = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
     if (j > 256 || rows_of(L) >= (int64_t)1 << 29) {  // tile does not fit registers / 32-bit offsets
@@ -1543,7 +1543,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     CHECK(check_ptr(y, "y"));
     CHECK(check_ptr(ws, "ws"));
     if (!h_dev) return fail(NKV_EINVAL, "h_dev is NULL");
-    if (j < 1) return fail(NKV_EINVAL, "j=%d < 1", j);
+    if (j < 1 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 1..%d", j, NKV_MAX_COLS);
     if ((flags & NKV_X_IS_LAST) && x != Q + (int64_t)(j - 1) * L->ld)
         return fail(NKV_EINVAL, "NKV_X_IS_LAST: x is not column j-1 of Q");
     hipStream_t st = S(stream);

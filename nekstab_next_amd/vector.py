@@ -41,6 +41,8 @@ class NekContext:
 
     def __init__(self, layout: NekLayout, weights=None, comm: Comm | None = None, max_cols: int = 256,
                  device: torch.device | int | None = None, time_in_dot: bool = False):
+        if not 1 <= max_cols < _lib.NKV_MAX_COLS:   # the closing multi-dot takes max_cols + 1 columns
+            raise ValueError(f"max_cols={max_cols} outside 1..{_lib.NKV_MAX_COLS - 1}")
         _lib.require_gpu()
         self.comm = comm if comm is not None else Comm()
         if layout.world != self.comm.world or layout.rank != self.comm.rank:

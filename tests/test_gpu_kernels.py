@@ -306,6 +306,13 @@ def test_shape_errors(gpu):
     for n_out in (0, 5):   # n_out outside [1, k]
         with pytest.raises(NkvError):
             ctx.call("nkv_rotate_cols", v.ptr, 4, ctx.h1.data_ptr(), 4, n_out, ctx.stream)
+    # more columns than a multi-dot's LDS partials hold: refused before any launch
+    with pytest.raises(NkvError, match="outside 1..1024"):
+        ctx.call("nkv_block_dot", ctx.w.data_ptr(), v.ptr, 1025, v.ptr, ctx.h1.data_ptr(), ctx.ws.data_ptr(), 0,
+                 ctx.stream)
+    with pytest.raises(NkvError, match="outside 1..1024"):
+        ctx.call("nkv_block_dot2", ctx.w.data_ptr(), v.ptr, 1025, v.ptr, v.ptr, ctx.h1.data_ptr(),
+                 ctx.ws.data_ptr(), 0, ctx.stream)
 
 
 @pytest.mark.parametrize("j", [1, 5, 8, 9, 31, 64, 65, 128, 129, 200, 256, 300])

@@ -96,6 +96,23 @@ def test_library_exports_every_header_symbol():
     assert lib.nkv_abi_version() == 1
 
 
+def test_header_constants_match_python():
+    from nekstab_next_amd import _lib
+
+    txt = open(os.path.join(ROOT, "include", "nekkrylov.h")).read()
+    defs = {k: int(v, 0) for k, v in re.findall(r"#define (NKV_[A-Z0-9_]+)\s+(0x[0-9a-f]+|\d+)u?", txt)}
+    for name in ("NKV_TILE", "NKV_MAX_COLS", "NKV_OK", "NKV_EINVAL", "NKV_EHIP", "NKV_ENAN", "NKV_ESHAPE",
+                 "NKV_TIME", "NKV_ACCUMULATE", "NKV_OVERWRITE", "NKV_NORM2", "NKV_TIME_DOT", "NKV_X_IS_LAST"):
+        assert defs[name] == getattr(_lib, name), name
+
+
+def test_context_rejects_too_many_columns():
+    from nekstab_next_amd.vector import NekContext
+
+    with pytest.raises(ValueError, match="max_cols"):
+        NekContext(NekLayout(ldim=2, lx1=4, lx2=2, nelgv=4), max_cols=1024)
+
+
 def test_workspace_size_is_host_only():
     from nekstab_next_amd import _lib
 
