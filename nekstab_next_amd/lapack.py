@@ -61,18 +61,21 @@ def eig(A: np.ndarray):
 
 
 def sort_eigendecomp(vals: np.ndarray, vecs: np.ndarray):
-    """Exchange sort by decreasing modulus; swaps only on strict ``norm(k) < norm(l)``."""
-    vals = vals.copy()
-    vecs = vecs.copy()
-    nrm = np.sqrt(vals.real ** 2 + vals.imag ** 2)
-    n = vals.shape[0]
+    """Exchange sort by decreasing modulus; swaps only on strict ``norm(k) < norm(l)``
+    (lapack_wrapper.f90:212-226).  The exchanges run on a permutation of Python floats (the same
+    float64 comparisons, so the same permutation, ties included) and are applied to the values
+    and vectors once."""
+    nrm = np.sqrt(vals.real ** 2 + vals.imag ** 2).tolist()
+    n = len(nrm)
+    idx = list(range(n))
     for k in range(n - 1):
+        nk = nrm[k]
         for l in range(k + 1, n):
-            if nrm[k] < nrm[l]:
-                nrm[[k, l]] = nrm[[l, k]]
-                vals[[k, l]] = vals[[l, k]]
-                vecs[:, [k, l]] = vecs[:, [l, k]]
-    return vals, vecs
+            if nk < nrm[l]:
+                nrm[k], nrm[l] = nrm[l], nk
+                idx[k], idx[l] = idx[l], idx[k]
+                nk = nrm[k]
+    return vals[idx], vecs[:, idx]
 
 
 def select_eigvals(wr: float, wi: float) -> bool:
