@@ -1123,6 +1123,78 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
+// Restart rotation for a few kept columns (n_out = NO <= NKV_ROTF_MAX, the Krylov–Schur case:
+// mstart-1 selected Schur vectors out of k): the multi-dot's streaming shape — every thread owns
+// P row pairs of a tile, walks the k columns U at a time with 16-byte non-temporal loads (1 KiB
+// per wave instruction, each column read in kThreads*P*16-byte runs), and keeps NO accumulators
+// per row; V[c, 0:NO] is wave-uniform (scalar loads).  2 N k NO flop against 8 N (k + NO) bytes:
+// at NO <= 8 this is HBM-bound on the VALU, where the MFMA tile would waste 16-NO of its 16
+// output columns and read Q in 128-byte pieces.  All k inputs of a row are consumed before its NO
+// outputs are stored and no other thread touches that row, so in place is safe.
+// ------------------------------------------------------------------------------------------
+#ifndef NKV_ROTF_MAX
+#define NKV_ROTF_MAX 8   // 0: never use the few-column rotation
+#endif
+#ifndef NKV_ROTF_P
+#define NKV_ROTF_P 4
+#endif
+#ifndef NKV_ROTF_U
+#define NKV_ROTF_U 4
+#endif
+static_assert(NKV_TILE % (kThreads * NKV_ROTF_P * 2) == 0, "rotate-few tile must divide the padding");
+template <int NO, int P, int U>
+__global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q, int64_t ld, int k,
+                                                         const double* __restrict__ V, int ldv, int64_t n_tiles) {
+    constexpr int kTile = kThreads * P * 2;
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int64_t r0 = t * kTile + 2 * threadIdx.x;
+        const double* qb = Q + r0;
+        double2 acc[NO][P];
+#pragma unroll
+        for (int o = 0; o < NO; ++o)
+#pragma unroll
+            for (int p = 0; p < P; ++p) acc[o][p] = make_double2(0.0, 0.0);
+        int c = 0;
+        for (; c + U <= k; c += U) {
+            double2 q[U][P];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int p = 0; p < P; ++p) q[u][p] = ldq(qb + (int64_t)(c + u) * ld + p * 2 * kThreads);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    const double v = V[c + u + (int64_t)o * ldv];
+#pragma unroll
+                    for (int p = 0; p < P; ++p) {
+                        acc[o][p].x = fma(q[u][p].x, v, acc[o][p].x);
+                        acc[o][p].y = fma(q[u][p].y, v, acc[o][p].y);
+                    }
+                }
+        }
+        for (; c < k; ++c) {
+            double2 q[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) q[p] = ldq(qb + (int64_t)c * ld + p * 2 * kThreads);
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                const double v = V[c + (int64_t)o * ldv];
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    acc[o][p].x = fma(q[p].x, v, acc[o][p].x);
+                    acc[o][p].y = fma(q[p].y, v, acc[o][p].y);
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < NO; ++o)
+#pragma unroll
+            for (int p = 0; p < P; ++p) st2s(Q + (int64_t)o * ld + r0 + p * 2 * kThreads, acc[o][p]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // synthetic operators and data
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__ d,
@@ -1733,6 +1805,18 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
     return NKV_OK;
 }
 
+extern "C++" template <int NO>
+static int launch_rotate_few(const nkv_layout* L, double* Q, int k, const double* V, int ldv, void* stream) {
+    constexpr int P = NKV_ROTF_P, U = NKV_ROTF_U;
+    const int64_t n_tiles = rows_of(L) / (kThreads * P * 2);
+    if (n_tiles < 1) return NKV_OK;
+    const int64_t g = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
+    hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)g), dim3(kThreads), 0, S(stream), Q, L->ld, k, V,
+                       ldv, n_tiles);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
 int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out, void* stream) {
     CHECK(check_layout(L));
     CHECK(check_ptr(Q, "Q"));
@@ -1741,6 +1825,19 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
     if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
     if (n_out < 1 || n_out > k) return fail(NKV_EINVAL, "rotate: n_out=%d outside [1, k=%d]", n_out, k);
     if (NKV_ROT_VALU && n_out == k) return rotate_valu(L, Q, k, V_dev, ldv, stream);
+    if (n_out <= NKV_ROTF_MAX) {
+        switch (n_out) {
+            case 1: return launch_rotate_few<1>(L, Q, k, V_dev, ldv, stream);
+            case 2: return launch_rotate_few<2>(L, Q, k, V_dev, ldv, stream);
+            case 3: return launch_rotate_few<3>(L, Q, k, V_dev, ldv, stream);
+            case 4: return launch_rotate_few<4>(L, Q, k, V_dev, ldv, stream);
+            case 5: return launch_rotate_few<5>(L, Q, k, V_dev, ldv, stream);
+            case 6: return launch_rotate_few<6>(L, Q, k, V_dev, ldv, stream);
+            case 7: return launch_rotate_few<7>(L, Q, k, V_dev, ldv, stream);
+            case 8: return launch_rotate_few<8>(L, Q, k, V_dev, ldv, stream);
+            default: break;
+        }
+    }
     if (NKV_ROT_STREAM && rows_of(L) % ((int64_t)NKV_ROT_WAVES * NKV_ROT_NB * 16) == 0) {
         const int kp = ((k + 31) & ~31) + 2;
         const int nact = (n_out + 15) / 16;

@@ -205,7 +205,8 @@ def test_rotate_vs_oracle(gpu, k):
     np.testing.assert_array_equal(syn.to_reference_order(lay, got[k]), Qref[k])  # column k untouched
 
 
-@pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 20), (129, 17), (256, 255), (300, 150), (576, 33)])
+@pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 6), (128, 8), (9, 9), (4, 4), (131, 5), (576, 7),
+                                     (128, 20), (129, 17), (256, 255), (300, 150), (576, 33)])
 def test_rotate_cols_vs_oracle(gpu, k, n_out):
     """Partial restart rotation: Q[:, :n_out] = Q[:, :k] V[:, :n_out]; columns n_out..k untouched."""
     lay = LAYOUTS["2d"]

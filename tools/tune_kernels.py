@@ -62,6 +62,12 @@ VARIANTS = {
     "d2_b768": {"NKV_D2_MAXB": 768},
     "d2_b512": {"NKV_D2_MAXB": 512},
     "d2_b256": {"NKV_D2_MAXB": 256},
+    "dc_u16": {"NKV_DC_U": 16},
+    "rotf_off": {"NKV_ROTF_MAX": 0},
+    "rotf_p2u8": {"NKV_ROTF_P": 2, "NKV_ROTF_U": 8},
+    "rotf_p8u2": {"NKV_ROTF_P": 8, "NKV_ROTF_U": 2},
+    "rotf_p1u16": {"NKV_ROTF_P": 1, "NKV_ROTF_U": 16},
+    "dc_g2048": {"NKV_DC_G": 2048},
     "dc_g256": {"NKV_DC_G": 256},
     "dc_g512": {"NKV_DC_G": 512},
     "dc_g768": {"NKV_DC_G": 768},
@@ -157,6 +163,7 @@ def run(names, E, rounds, js, only=None):
                                                     None, 0, st), 16.0 * N),
             "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
             "rotate": (lambda: L.nkv_rotate(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, st), 16.0 * j * N),
+            "rotate_6": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, 6, st), 8.0 * (j + 6) * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
         }
