@@ -30,10 +30,13 @@ def main():
           "event brackets include the ~5 us second-stage reduction kernel)")
     rs = bench.get("restart")
     if rs:
-        # restart rotations: k_rotate_stream<NB, MB, W, U>, MB = ceil(n_out / 16) column blocks
-        mb_kept = (rs["mstart"] - 1 + 15) // 16
-        for label, mb, ms in (("rotate kept", mb_kept, rs["rotate_kept_ms"]), ("rotate full", 8, rs["rotate_full_ms"])):
-            rows = [r for r in stats if f"k_rotate_stream<1, {mb}," in r["Name"]]
+        # restart rotations: n_out <= 8 kept columns run k_rotate_few<n_out, P, U>, wider ones
+        # k_rotate_stream<NB, MB, W, U> with MB = ceil(n_out / 16) column blocks
+        n_kept = rs["mstart"] - 1
+        kept_key = f"k_rotate_few<{n_kept}," if n_kept <= 8 else f"k_rotate_stream<1, {(n_kept + 15) // 16},"
+        for label, key, ms in (("rotate kept", kept_key, rs["rotate_kept_ms"]),
+                               ("rotate full", "k_rotate_stream<1, 8,", rs["rotate_full_ms"])):
+            rows = [r for r in stats if key in r["Name"]]
             if rows:
                 calls = sum(int(r["Calls"]) for r in rows)
                 avg = sum(float(r["TotalDurationNs"]) for r in rows) / calls / 1e6

@@ -24,9 +24,9 @@ FAMILIES = {
     "finish": ("k_finish",),
     "op_diag": ("k_op_diag",),
     "copy": ("k_blas1<1>",),
-    # restart rotations of bench.py's restart leg (8 B/lane loads: the x2 FETCH correction is for
-    # 16 B/lane reads, so these rows show how far the correction holds for narrower loads)
-    "rotate_kept": ("k_rotate_stream<1, 1,",),
+    # restart rotations of bench.py's restart leg (k_rotate_few: 16 B/lane loads; k_rotate_stream:
+    # 8 B/lane loads, so its rows show how far the x2 FETCH correction holds for narrower loads)
+    "rotate_kept": ("k_rotate_few<", "k_rotate_stream<1, 1,"),
     "rotate_full": ("k_rotate_stream<1, 8,",),
 }
 
