@@ -67,7 +67,8 @@ namespace {
 #define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
 #endif
 #ifndef NKV_D2_MAXB
-#define NKV_D2_MAXB NKV_MAXB  // workgroups of the two-vector multi-dot
+#define NKV_D2_MAXB 256  // workgroups of the two-vector multi-dot: one per CU (+1 % over 1024 at
+                          // N=1e8 and at the 8-GPU shard; 384 = 1.5 per CU loses 6-10 %)
 #endif
 #ifndef NKV_D2_FIELDLOOP
 #define NKV_D2_FIELDLOOP 1  // two-vector multi-dot: one block walks all weighted fields of a tile

@@ -62,6 +62,8 @@ VARIANTS = {
     "d2_b768": {"NKV_D2_MAXB": 768},
     "d2_b512": {"NKV_D2_MAXB": 512},
     "d2_b256": {"NKV_D2_MAXB": 256},
+    "d2_b384": {"NKV_D2_MAXB": 384},
+    "d2_b1024": {"NKV_D2_MAXB": 1024},
     "dc_u16": {"NKV_DC_U": 16},
     "rotf_off": {"NKV_ROTF_MAX": 0},
     "rotf_p2u8": {"NKV_ROTF_P": 2, "NKV_ROTF_U": 8},
