@@ -61,7 +61,9 @@ namespace {
 #define NKV_DC_EXPERIMENT 0
 #endif
 #ifndef NKV_DC_G
-#define NKV_DC_G NKV_MAXB  // workgroups of the DCGS2 dual update
+#define NKV_DC_G 768  // workgroups of the DCGS2 dual update: 3 per CU (122 VGPRs allow 4) is 1-6 %
+                      // faster than 4 per CU at N=1e8 and at the 8-GPU shard; non-multiples of the
+                      // 256 CUs lose 5-10 % (profiles/r01k_tune_update_grid.log)
 #endif
 #ifndef NKV_DC_FIELDLOOP
 #define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
@@ -1302,7 +1304,10 @@ __global__ __launch_bounds__(kThreads) void k_fill_hash(double* __restrict__ x, 
     if (blockIdx.x == 0 && threadIdx.x == 0) x[time_off] = 0.0;
 }
 
-int grid_for(int64_t work_items, int cap = 4096) {
+#ifndef NKV_STREAM_G
+#define NKV_STREAM_G 4096  // workgroup cap of the streaming kernels (op_diag, finish, BLAS-1)
+#endif
+int grid_for(int64_t work_items, int cap = NKV_STREAM_G) {
     int64_t g = (work_items + kThreads - 1) / kThreads;
     if (g < 1) g = 1;
     if (g > cap) g = cap;

@@ -73,6 +73,12 @@ VARIANTS = {
     "dc_g256": {"NKV_DC_G": 256},
     "dc_g512": {"NKV_DC_G": 512},
     "dc_g768": {"NKV_DC_G": 768},
+    "dc_g640": {"NKV_DC_G": 640},
+    "dc_g1024": {"NKV_DC_G": 1024},
+    "st_g2048": {"NKV_STREAM_G": 2048},
+    "st_g1024": {"NKV_STREAM_G": 1024},
+    "st_g768": {"NKV_STREAM_G": 768},
+    "dc_g896": {"NKV_DC_G": 896},
 }
 
 
