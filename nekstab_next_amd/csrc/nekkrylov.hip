@@ -81,6 +81,15 @@ namespace {
 #ifndef NKV_FUSE_PF
 #define NKV_FUSE_PF 0  // 1: prefetch the next tile's columns across the per-tile barrier
 #endif
+#ifndef NKV_DC_SYNC
+#define NKV_DC_SYNC 0  // experiment: align the dual update's store phases over the grid (soft barrier)
+#endif
+#ifndef NKV_DC_SYNC_US
+#define NKV_DC_SYNC_US 20  // ... longest wait per round (us) before a block stores anyway
+#endif
+#ifndef NKV_XCD_MAP
+#define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
+#endif
 
 constexpr int kThreads = 256;                       // 4 waves of 64
 constexpr int kStreamUnr = NKV_STREAM_UNR;
@@ -91,6 +100,16 @@ constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots 
 constexpr int kColUnroll = NKV_COLU;                 // columns in flight per thread (block dot)
 constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
 constexpr int kRotMaxK = 576;                        // rotation: 64-row tiles up to k=256, 32-row beyond
+
+// Tile order of a grid-stride loop.  Blocks b and b+8 share an XCD (round-robin dispatch,
+// MI355X_MICROARCH.md §Workgroup dispatch); with NKV_XCD_MAP the G/8 blocks of one XCD take
+// consecutive tiles of every round.  A permutation of [0, G): speed only, any placement is correct.
+__device__ __forceinline__ int tile_block(int b, int G) {
+#if NKV_XCD_MAP
+    if ((G & 7) == 0) return (b & 7) * (G >> 3) + (b >> 3);
+#endif
+    return b;
+}
 
 thread_local char g_err[512] = "";
 
@@ -516,7 +535,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+    for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_per_field; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
@@ -681,6 +700,20 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
     }
 }
 
+// Timing alignment only (NKV_DC_SYNC experiment): a block counts itself in and waits until
+// `target` blocks have arrived or NKV_DC_SYNC_US microseconds have passed, whichever is first, so
+// the wait always ends (no co-residency assumption) and no data crosses it.
+__device__ __forceinline__ void soft_barrier(int* ctr, int target) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+               __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)NKV_DC_SYNC_US * 100)
+            __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+}
+
 // DCGS2 update, one read of Q_m (m columns):  qbar = (u s - Q_m a) * rinv  -> column m (in place),
 // f = (A u) s rinv - Q_m x - qbar * yc  -> fout (the next column: normalised one step later),
 // ||f||_W^2 partial.  One row tile (kTile rows at r0): returns f in af.
@@ -689,7 +722,8 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
                                            const double* __restrict__ a, const double* __restrict__ x,
                                            double rinv, double yc, double sc, double* __restrict__ qj,
                                            const double* __restrict__ win, double* __restrict__ f,
-                                           int64_t r0, double2 (&af)[kPairs]) {
+                                           int64_t r0, double2 (&af)[kPairs], int* sync = nullptr,
+                                           int sync_target = 0) {
     double2 aq[kPairs];
     const double wsc = sc * rinv;
 #pragma unroll
@@ -731,6 +765,7 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
             af[k].y = fma(xc, q.y, af[k].y);
         }
     }
+    if (sync) soft_barrier(sync, sync_target);
 #pragma unroll
     for (int k = 0; k < kPairs; ++k) {
         const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
@@ -781,8 +816,21 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
     }
     double2 af[kPairs];
     if constexpr (!kNrm) {
-        for (int t = blockIdx.x; t < tiles_total; t += gridDim.x)
+#if NKV_DC_SYNC
+        int* sync = reinterpret_cast<int*>(partials) - 16;   // the workspace's sync word (zeroed per launch)
+        const int rounds = (tiles_total + gridDim.x - 1) / gridDim.x;
+        for (int r = 0; r < rounds; ++r) {
+            const int t = tile_block(blockIdx.x, gridDim.x) + r * gridDim.x;
+            if (t < tiles_total)
+                dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af,
+                                   sync, (r + 1) * gridDim.x);
+            else
+                soft_barrier(sync, (r + 1) * gridDim.x);
+        }
+#else
+        for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_total; t += gridDim.x)
             dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af);
+#endif
         return;
     }
     double nrm = 0.0;
@@ -791,7 +839,7 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
     // not once per field), then the pressure tiles one by one
     const int n_wf = tiles_per_field > 0 ? tiles_w / tiles_per_field : 0;
     const int n_units = tiles_per_field + (tiles_total - tiles_w);
-    for (int u = blockIdx.x; u < n_units; u += gridDim.x) {
+    for (int u = tile_block(blockIdx.x, gridDim.x); u < n_units; u += gridDim.x) {
         if (u < tiles_per_field) {
             double2 wv[kPairs];
 #pragma unroll
@@ -1205,7 +1253,7 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
                                                       double* __restrict__ y, int64_t rows,
                                                       int64_t time_off, double ts) {
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
-    for (int64_t ci = blockIdx.x; ci < chunks; ci += gridDim.x) {
+    for (int64_t ci = tile_block(blockIdx.x, gridDim.x); ci < chunks; ci += gridDim.x) {
         const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
         double2 dv[kStreamUnr], xv[kStreamUnr];
 #pragma unroll
@@ -1693,6 +1741,9 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
+#if NKV_DC_SYNC
+    if (!nrm2_dev) NKV_HIP(hipMemsetAsync(reinterpret_cast<int*>(part) - 16, 0, sizeof(int), st));
+#endif
     auto kern = large ? (nrm2_dev ? k_dcgs2_update<NKV_DC_PAIRS, true> : k_dcgs2_update<NKV_DC_PAIRS, false>)
                       : (nrm2_dev ? k_dcgs2_update<NKV_PAIRS_SMALL, true> : k_dcgs2_update<NKV_PAIRS_SMALL, false>);
     hipLaunchKernelGGL(kern, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj, win, fout, w, L->sv, tpf,

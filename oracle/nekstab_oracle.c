@@ -307,10 +307,20 @@ int orc_select_eigenvalues(int n, const double* re, const double* im, double del
     double* arr = (double*)malloc(sizeof(double) * (size_t)n);
     memcpy(arr, mod, sizeof(double) * (size_t)n);
     orc_quicksort2(n, arr, idx);
+    /* k_dim < nev+4 would index idx(0) and below (out of bounds in the reference too): refused,
+     * as the product does; at k_dim == nev+4 the conjugate check has no idx(0) to look at. */
+    if (n - (nev + 4) < 0) {
+        free(idx);
+        free(mod);
+        free(arr);
+        return -1;
+    }
     for (int i = 0; i < n; ++i) selected[i] = mod[i] >= (1.0 - delta);
     for (int p = n - (nev + 3); p <= n; ++p) selected[idx[p - 1] - 1] = 1; /* idx(n-(nev+3):n) */
-    const int a = idx[n - (nev + 3) - 1] - 1, b = idx[n - (nev + 4) - 1] - 1;
-    if (im[a] == -im[b]) selected[b] = 1;
+    if (n - (nev + 4) >= 1) {
+        const int a = idx[n - (nev + 3) - 1] - 1, b = idx[n - (nev + 4) - 1] - 1;
+        if (im[a] == -im[b]) selected[b] = 1;
+    }
     int cnt = 0;
     for (int i = 0; i < n; ++i) cnt += selected[i] ? 1 : 0;
     free(idx);

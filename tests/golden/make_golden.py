@@ -1,0 +1,221 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures under tests/golden/ (run in the build container; committed output).
+
+Provenance, per fixture:
+
+* ``fld_headers.json`` — the four Nek5000 base-flow files the reference ships
+  (``examples/cylinder/BF_1cyl0.f00001``, ``BFRe40_1cyl0.f00001``,
+  ``examples/back_fstep/{baseflow,transient_growth}/BF_bfs0.f00001``), parsed HERE by an
+  independent byte-offset reader (``_parse_std`` below, not ``nekstab_next_amd.fld``): header
+  tokens, endian tag, element-map checksum and per-field sum / sum of squares / min / max.
+  Data held by the reference itself: these pin the product's ``.fld`` reader.
+* ``bf_1cyl0_seed.npz`` — the cylinder base flow (U, V and P mapped to the lx2 mesh) of
+  ``BF_1cyl0.f00001`` as one state vector on the real cylinder mesh (E=1996, N=175,648, reference
+  order), the seed of the config-2 golden run; lets the GPU box run on the reference's own data
+  without ``/root/reference``.
+* ``ks_*.npz`` / ``gmres_*.npz`` — outputs of the CPU oracle (``oracle/``: the C restatement of
+  ``update_hessenberg_matrix`` and the numpy/SciPy-LAPACK restatement of the drivers) on the
+  synthetic BASELINE operators.  The reference's Fortran is not buildable in this image (DESIGN.md
+  §3), so these are oracle outputs, not reference outputs: they freeze the oracle (a change to it
+  shows up as a fixture mismatch) and let the GPU tests check the HIP path without running the
+  oracle.  Parity against the reference itself stays "unpinned" (DESIGN.md §3).
+* ``ordering.npz`` — inputs/outputs of the C transliteration of ``quicksort2``
+  (core/utils.f90:29-138), ``select_eigenvalues`` (core/eigensolvers.f90:688-754) and
+  ``sort_eigendecomp`` (core/lapack_wrapper.f90:181-228), including the pivot defect.
+
+usage: python tests/golden/make_golden.py        (writes next to this file)
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+REF = "/root/reference"
+FLD_FILES = [
+    "examples/cylinder/BF_1cyl0.f00001",
+    "examples/cylinder/BFRe40_1cyl0.f00001",
+    "examples/back_fstep/baseflow/BF_bfs0.f00001",
+    "examples/back_fstep/transient_growth/BF_bfs0.f00001",
+]
+
+
+def _parse_std(path):
+    """Byte-offset parse of a Nek5000 '#std' file: 132-byte ASCII header, 4-byte endian tag
+    (6.54321 as float32), nel int32 element ids, then per element group the data, X/U as ldim
+    blocks per element, P/T one block per element."""
+    raw = open(path, "rb").read()
+    tok = raw[:132].decode("ascii").split()
+    wd, nx, ny, nz, nel = (int(t) for t in tok[1:6])
+    rd = tok[11]
+    tag_le = struct.unpack("<f", raw[132:136])[0]
+    bo = "<" if abs(tag_le - 6.54321) < 1e-5 else ">"
+    emap = np.array(struct.unpack(f"{bo}{nel}i", raw[136:136 + 4 * nel]), dtype=np.int64)
+    pts = nx * ny * nz
+    ldim = 3 if nz > 1 else 2
+    off = 136 + 4 * nel
+    fmt = "d" if wd == 8 else "f"
+    fields = {}
+    for g in rd:
+        ncomp = ldim if g in "XU" else 1
+        cnt = nel * ncomp * pts
+        vals = np.array(struct.unpack(f"{bo}{cnt}{fmt}", raw[off:off + cnt * wd]), dtype=np.float64)
+        off += cnt * wd
+        blk = vals.reshape(nel, ncomp, pts)
+        names = {"X": ["x", "y", "z"], "U": ["vx", "vy", "vz"], "P": ["pr"], "T": ["t"]}[g]
+        for c in range(ncomp):
+            fields[names[c]] = blk[:, c, :]
+    assert off == len(raw), (path, off, len(raw))
+    return tok, tag_le, emap, fields
+
+
+def gen_fld():
+    out = {}
+    for rel in FLD_FILES:
+        tok, tag, emap, fields = _parse_std(os.path.join(REF, rel))
+        out[rel] = {
+            "header_tokens": tok[:12],
+            "size_bytes": os.path.getsize(os.path.join(REF, rel)),
+            "endian_tag": tag,
+            "emap_sum": int(emap.sum()), "emap_first": emap[:8].tolist(),
+            "emap_sha1": hashlib.sha1(emap.astype("<i8").tobytes()).hexdigest(),
+            "fields": {k: {"sum": float(v.sum()), "sumsq": float((v * v).sum()), "min": float(v.min()),
+                           "max": float(v.max()), "elem0": v[0].tolist()} for k, v in fields.items()},
+        }
+    json.dump(out, open(os.path.join(HERE, "fld_headers.json"), "w"), indent=1)
+
+
+def _checksum(a):
+    return np.array([np.sum(a), np.sum(a * a), a[0], a[-1]])
+
+
+def gen_solvers():
+    import oracle as orc
+    from helpers import olayout, oracle_diag_matvec, oracle_rot2_matvec
+    from nekstab_next_amd import fld
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import NekLayout, box3d_layout, cylinder_layout
+
+    orc.set_threads(8)
+
+    def seed_of(lay, L, w, s):
+        return orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, s)))
+
+    # config 1: 2-D lx1=6, E=1136 (N=99,968), diag spectrum, Krylov–Schur k_dim=16, schur_tgt=5
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=1136)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    d, exact = syn.diag_spectrum(lay)
+    dref = syn.to_reference_order(lay, d)
+    q1 = seed_of(lay, L, w, 11)
+    r = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
+    np.savez(os.path.join(HERE, "ks_config1.npz"), vals=r["vals"], residual=r["residual"],
+             mstart=np.array(r["mstart"]), cnt=np.array(r["cnt"]), schur_cnt=r["schur_cnt"],
+             H_first=r["H_first"], H_final=r["H"], seed_checksum=_checksum(q1), d_checksum=_checksum(dref),
+             w_checksum=_checksum(w), exact=exact)
+
+    # config 2 on the real cylinder mesh (E=1996, N=175,648) seeded with the reference's own base
+    # flow BF_1cyl0.f00001 (U, V, P); rotation-scaling operator, Krylov–Schur schur_tgt=2 (1cyl.usr:15)
+    # at k_dim=16 (two restarts through conjugate pairs) and k_dim=64 (BASELINE's m, no restart)
+    lay = cylinder_layout(1996)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    f = fld.read_fld(os.path.join(REF, FLD_FILES[0]))
+    bf = syn.to_reference_order(lay, fld.vector_from_fld(lay, f))
+    np.savez_compressed(os.path.join(HERE, "bf_1cyl0_seed.npz"), seed_ref=bf)
+    q1 = orc.prepare_seed(L, w, bf)
+    c, s, dr, exact = syn.rot2_operator(lay)
+    for k in (16, 64):
+        r = orc.krylov_schur(L, w, oracle_rot2_matvec(lay, c, s, dr), q1, k, 2)
+        np.savez(os.path.join(HERE, f"ks_config2_bf_k{k}.npz"), vals=r["vals"], residual=r["residual"],
+                 mstart=np.array(r["mstart"], dtype=np.int64), cnt=np.array(r["cnt"]), schur_cnt=r["schur_cnt"],
+                 H_first=r["H_first"], seed_checksum=_checksum(q1), exact=exact)
+
+    # config 3 family, reduced (box3d E=40, N=90,592): plain 40-step Arnoldi on the shift-invert
+    # Laplacian (|mu| from 0.1 to 3e8: the strongly graded spectrum of the headline config)
+    lay = box3d_layout(40)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    d, exact = syn.laplacian_shift_invert(lay)
+    q1 = seed_of(lay, L, w, 11)
+    r = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 40, 0)
+    np.savez(os.path.join(HERE, "ks_config3_arnoldi.npz"), vals=r["vals"], residual=r["residual"],
+             H=r["H"], seed_checksum=_checksum(q1), exact=exact[:64])
+
+    # config 4: ts_gmres on J = D - I (cylinder layout E=1996, the real mesh size), k_dim=200,
+    # maxiter=10, tol=1e-9 (1cyl.usr:14, newton_krylov.f90:44, 1cyl.par:18,23)
+    lay = cylinder_layout(1996)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    d, _ = syn.diag_spectrum(lay)
+    J = syn.to_reference_order(lay, d) - 1.0
+    rhs = syn.to_reference_order(lay, syn.hash_vector(lay, 3))
+
+    def mv(x, y):
+        y[:] = J * x
+        y[-1] = 0.0
+
+    sol, hist = orc.ts_gmres(L, w, mv, rhs, maxiter=10, ksize=200, tol=1e-9)
+    np.savez(os.path.join(HERE, "gmres_config4.npz"), outer=np.array(hist["outer"]),
+             inner=np.array(hist["inner"]), y_last=hist["y"][-1], sol_checksum=_checksum(sol), sol_head=sol[:256], sol_wnorm2=orc.k_dot(L, w, sol, sol),
+             rhs_checksum=_checksum(rhs))
+    orc.set_threads(1)
+
+
+def gen_ordering():
+    import oracle as orc
+
+    rng = np.random.default_rng(2024)
+    qs_in, qs_idx, qs_out = [], [], []
+    for n in list(range(1, 41)) + [64, 100, 128]:
+        for rep in range(3):
+            a = rng.standard_normal(n) * (10.0 ** rng.integers(-3, 3))
+            if rep == 2 and n > 3:
+                a[rng.integers(0, n, size=n // 3)] = a[0]   # ties
+            idx, srt = orc.quicksort2(a)
+            qs_in.append(a)
+            qs_idx.append(idx)
+            qs_out.append(srt)
+    # the documented defect: [3,1,2,0.5,7,6,5,4] loses an index
+    sel_vals, sel_mask, sel_cnt, sel_args = [], [], [], []
+    for n in (8, 9, 16, 24, 40, 64, 128):   # n >= nev + 4 (the reference indexes idx(n-(nev+4)))
+        for rep in range(4):
+            if n < 2 + rep + 4:
+                continue
+            nr = n // 2
+            re = rng.uniform(-1.1, 1.1, nr)
+            pairs = (n - nr) // 2
+            z = rng.uniform(0.2, 1.05, pairs) * np.exp(1j * rng.uniform(0.05, 3.0, pairs))
+            v = np.concatenate([re + 0j, z, np.conj(z)])
+            v = np.concatenate([v, np.zeros(n - v.size)])
+            rng.shuffle(v)
+            delta, nev = (0.1, 2 + rep)
+            mask, cnt = orc.select_eigenvalues(v, delta, nev)
+            sel_vals.append(v)
+            sel_mask.append(mask)
+            sel_cnt.append(cnt)
+            sel_args.append((delta, nev))
+    pad = lambda xs, dt: np.array([np.pad(x, (0, 128 - len(x))) for x in xs], dtype=dt)  # noqa: E731
+    np.savez(os.path.join(HERE, "ordering.npz"),
+             qs_len=np.array([len(a) for a in qs_in]), qs_in=pad(qs_in, np.float64),
+             qs_idx=pad(qs_idx, np.int64), qs_out=pad(qs_out, np.float64),
+             sel_len=np.array([len(v) for v in sel_vals]), sel_vals=pad(sel_vals, np.complex128),
+             sel_mask=pad(sel_mask, bool), sel_cnt=np.array(sel_cnt), sel_args=np.array(sel_args))
+
+
+if __name__ == "__main__":
+    gen_fld()
+    gen_ordering()
+    gen_solvers()
+    for n in sorted(os.listdir(HERE)):
+        print(f"{os.path.getsize(os.path.join(HERE, n)):10d}  {n}")

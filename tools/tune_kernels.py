@@ -79,6 +79,14 @@ VARIANTS = {
     "st_g1024": {"NKV_STREAM_G": 1024},
     "st_g768": {"NKV_STREAM_G": 768},
     "dc_g896": {"NKV_DC_G": 896},
+    "xcd": {"NKV_XCD_MAP": 1},
+    "xcd_dcg1024": {"NKV_XCD_MAP": 1, "NKV_DC_G": 1024},
+    "xcd_d2b512": {"NKV_XCD_MAP": 1, "NKV_D2_MAXB": 512},
+    "xcd_d2b1024": {"NKV_XCD_MAP": 1, "NKV_D2_MAXB": 1024},
+    "dc_sync": {"NKV_DC_SYNC": 1},
+    "dc_sync5": {"NKV_DC_SYNC": 1, "NKV_DC_SYNC_US": 5},
+    "dc_sync_g512": {"NKV_DC_SYNC": 1, "NKV_DC_G": 512},
+    "dc_sync_g256": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256},
 }
 
 
