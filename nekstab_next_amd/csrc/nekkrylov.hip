@@ -87,6 +87,10 @@ namespace {
 #ifndef NKV_DC_SYNC_US
 #define NKV_DC_SYNC_US 20  // ... longest wait per round (us) before a block stores anyway
 #endif
+#ifndef NKV_ST_AUX
+#define NKV_ST_AUX -1  // stores of the dual update / op_diag: -1 nontemporal global store; >= 0 buffer
+                       // store with this cache policy (1 sc0, 2 nt, 16 sc1, 17 sc0 sc1, 18 nt sc1)
+#endif
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
@@ -222,6 +226,18 @@ __device__ __forceinline__ double2 ldq(const double* p) {
 #endif
 }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+// Store of one double2 at element offset `off` (< 2^29) of a streamed vector `base` (wave-uniform),
+// with the cache policy NKV_ST_AUX (a buffer store; -1: st2s below).
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st2s(double* p, double2 v);
+__device__ __forceinline__ void st2p(double* base, int64_t off, double2 v) {
+#if NKV_ST_AUX >= 0
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xFFFFFFFFu, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, v), r, (int)(off * 8), 0, NKV_ST_AUX);
+#else
+    st2s(base + off, v);
+#endif
+}
 // Stores of whole streamed vectors (800 MB at N=1e8, never re-read from cache): non-temporal (NKV_NT_ST)
 __device__ __forceinline__ void st2s(double* p, double2 v) {
 #if NKV_NT_ST
@@ -775,11 +791,11 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
 #if NKV_DC_EXPERIMENT >= 1
         if (af[k].x == 12345.678)
 #endif
-        st2s(qj + r0 + k * 2 * kThreads, qbv);
+        st2p(qj, r0 + k * 2 * kThreads, qbv);
 #if NKV_DC_EXPERIMENT == 1
         if (af[k].x == 12345.678)
 #endif
-        st2s(f + r0 + k * 2 * kThreads, af[k]);
+        st2p(f, r0 + k * 2 * kThreads, af[k]);
     }
 }
 
@@ -1263,7 +1279,7 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < kStreamUnr; ++u)
-            st2s(y + 2 * (p0 + u * kThreads), make_double2(dv[u].x * xv[u].x, dv[u].y * xv[u].y));
+            st2p(y, 2 * (p0 + u * kThreads), make_double2(dv[u].x * xv[u].x, dv[u].y * xv[u].y));
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
 }

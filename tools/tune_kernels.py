@@ -87,6 +87,13 @@ VARIANTS = {
     "dc_sync5": {"NKV_DC_SYNC": 1, "NKV_DC_SYNC_US": 5},
     "dc_sync_g512": {"NKV_DC_SYNC": 1, "NKV_DC_G": 512},
     "dc_sync_g256": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256},
+    "st_buf0": {"NKV_ST_AUX": 0},
+    "st_sc0": {"NKV_ST_AUX": 1},
+    "st_nt": {"NKV_ST_AUX": 2},
+    "st_sc1": {"NKV_ST_AUX": 16},
+    "st_sc0sc1": {"NKV_ST_AUX": 17},
+    "st_ntsc1": {"NKV_ST_AUX": 18},
+    "st_all": {"NKV_ST_AUX": 19},
 }
 
 
