@@ -61,11 +61,12 @@ def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,E_box,E_cyl", [(2, 96, 400), (3, 97, 401)])
+@pytest.mark.parametrize("world,E_box,E_cyl", [(2, 96, 400), (3, 97, 401), (8, 101, 403)])
 def test_ranks_match_one_rank(gpu, world, E_box, E_cyl):
     """Krylov–Schur on `world` gloo ranks sharing the GPU (the sharded HIP path, one shard per
     process) reproduces the one-rank run; (3, 97, 401) gives ragged shards (32/32/33 and
-    133/134/134 elements)."""
+    133/134/134 elements); (8, 101, 403) rehearses the 8-way split of the driver's 8-GPU run with
+    ragged shards (12/13 and 50/51 elements)."""
     mgr = mp.Manager()
     out = mgr.dict()
     ctx = mp.get_context("spawn")
