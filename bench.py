@@ -52,10 +52,11 @@ def survey_model_bytes(N, N_w, n_v, m):
     return tot
 
 
-def executed_bytes(N, N_w, n_v, m, mode):
+def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
     """HBM bytes the executed algorithm moves per factorisation (global sizes), per kernel:
     block_dot 8(jN_w + N_w + n_v); fused update_dot 8(jN + 2N + n_v); update+norm 8(jN + 2N + n_v);
-    finish 8(2N); diag matvec 8(3N).  (PMC FETCH/WRITE_SIZE agree within 1%, profiles/.)"""
+    finish 8(2N); diag matvec 8(3N); DCGS2 dual update 8((j-1)N + 4N), over a lazy basis (one
+    output vector) 8(jN + 2N).  (PMC FETCH/WRITE_SIZE agree within 1%, profiles/.)"""
     tot = 0.0
     for j in range(1, m + 1):
         dot = 8.0 * (j * N_w + N_w + n_v)
@@ -65,7 +66,8 @@ def executed_bytes(N, N_w, n_v, m, mode):
         elif mode == "cgs2-unfused":
             tot += 2 * dot + upd + (upd + 8.0 * n_v)
         elif mode == "dcgs2":   # two-vector dot over j-1 streamed columns (+ u, A u); dual update over j-1
-            tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v) + 8.0 * ((j - 1) * N + 4 * N)
+            tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v)
+            tot += 8.0 * (j * N + 2 * N) if lazy else 8.0 * ((j - 1) * N + 4 * N)
         else:
             raise ValueError(mode)
         tot += (0.0 if mode == "dcgs2" else 8.0 * 2 * N) + 8.0 * 3 * N   # normalise pass (not in dcgs2) + matvec
@@ -142,6 +144,8 @@ def main():
     ap.add_argument("--E", type=int, default=44176, help="global elements (44,176 -> N=1.0e8)")
     ap.add_argument("--m", type=int, default=128)
     ap.add_argument("--mode", default="dcgs2", help="dcgs2 (default) | cgs2 | cgs2-unfused")
+    ap.add_argument("--lazy-basis", action="store_true",
+                    help="dcgs2 over a lazy basis Q = S T (one vector write less per step)")
     ap.add_argument("--cpu-E", type=int, default=512)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -185,9 +189,11 @@ def main():
     Hd = HessenbergDev(ctx, m)
     f = ctx.vector()
 
+    lazy = args.mode == "dcgs2" and args.lazy_basis
+
     def one_step():
         prepare_seed(seed, Q[0])
-        arnoldi_factorization(ctx, op, Q, Hd, 1, m, f=f, mode=args.mode)
+        arnoldi_factorization(ctx, op, Q, Hd, 1, m, f=f, mode=args.mode, lazy=lazy)
         H = Hd.download()
         vals, vecs = lapack.eig(H[:m, :m])
         res = np.abs(H[m, m - 1] * vecs[m - 1, :])
@@ -246,7 +252,7 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     nv_g = glay.pts_v * glay.nelgv
-    value = executed_bytes(glay.N, glay.N_w, nv_g, m, args.mode) * args.steps / elapsed / 1e9
+    value = executed_bytes(glay.N, glay.N_w, nv_g, m, args.mode, lazy) * args.steps / elapsed / 1e9
     effective = survey_model_bytes(glay.N, glay.N_w, nv_g, m) * args.steps / elapsed / 1e9
 
     # Ritz accuracy vs the exact spectrum of the synthetic operator
@@ -295,7 +301,7 @@ def main():
             "config": {
                 "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
                 "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
-                "m": m, "mode": args.mode, "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
+                "m": m, "mode": args.mode + ("-lazy" if lazy else ""), "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
                                 + " allreduce") if world > 1 else "single GPU",
             },
             "roofline": {

@@ -162,6 +162,25 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
                      double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream);
 
+/* DCGS2 over a LAZY basis (same replacement target): the finished q_j is never written.  The stored
+ * columns S_0..S_{m-1} keep the raw provisional vectors and the orthonormal basis is Q = S T with
+ * T upper triangular (device, column c at T + c*ldt, ldt >= m+1; T_0 empty, a finished column's
+ * T column = e_c).  Step j (m = j-1; S column m holds u; f = A u):
+ *   nkv_block_dot2(S, j, x=u, y=f) -> h                                            (all-reduce 2j)
+ *   nkv_dcgs2_coef_lazy(m, h, h+j, nrm, H, ldh, coef, T, ldt)   as nkv_dcgs2_coef after mapping the
+ *       raw dots by T_m^T; appends T column m; coef + 3m+5 = z (m+1 entries)
+ *   nkv_dcgs2_update_lazy(S, m, coef, f, S col j) -> S col j = (A u) s/r - S[:,0:m+1] z  (the next u)
+ * After the last step: nkv_block_dot(S, m+1, u) -> h, nkv_dcgs2_coef_lazy(m, h, NULL, h+m, ..., T),
+ * nkv_block_update(S, m, coef+3m+5, u), nkv_normalize_dev(u, coef+2m+3): column m final, T column
+ * m = e_m.  One output vector per update instead of two (8N bytes less per step); consumers fold T
+ * into their coefficients (restart rotation V -> T V, mode reconstruction y -> T y) or rotate the
+ * basis by T once (nkv_rotate_cols(S, L, T, ldt, L)). */
+int nkv_dcgs2_coef_lazy(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev,
+                        double* H_dev, int64_t ldh, double* coef_dev, double* T_dev, int64_t ldt, void* ws,
+                        void* stream);
+int nkv_dcgs2_update_lazy(const nkv_layout* L, const double* S, int m, const double* coef_dev, const double* win,
+                          double* fout, void* ws, unsigned flags, void* stream);
+
 /* ---- Krylov–Schur restart (a10, schur_condensation eigensolvers.f90:421-442) --------------
  * In place: Q[:,0:k] <- Q[:,0:k] * V, V k-by-k column-major (leading dim ldv) in device memory.
  * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 576. */

@@ -192,14 +192,79 @@ def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
     ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
 
 
+def _dcgs2_step_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool) -> None:
+    """``_dcgs2_step`` over a lazy basis (include/nekkrylov.h, nkv_dcgs2_coef_lazy): the stored
+    columns stay the raw provisional vectors, T gains column j-1, and the update writes only the
+    next u = (A u) s/r - S[:, 0:j] z — the finished q_j is never stored."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    m = j - 1
+    h = ctx.hd[: 2 * j]
+    hp, cp = h.data_ptr(), ctx.coef.data_ptr()
+    u = Q.col_ptr(m)
+    if tm:
+        tm.begin("block_dot2")
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, hp, ws, tf | NKV_X_IS_LAST, st)
+    if tm:
+        tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_dcgs2_coef_lazy", m, hp, hp + 8 * j, None if first else hp + 8 * m, Hd.t.data_ptr(),
+                Hd.k + 1, cp, Q.T.data_ptr(), Q.k, ws, st)
+    if tm:
+        tm.begin("dcgs2_update")
+    ctx.call("nkv_dcgs2_update_lazy", Q.ptr, m, cp, f.ptr, Q.col_ptr(j), ws, NKV_TIME, st)
+    if tm:
+        tm.end("dcgs2_update", 8.0 * ((m + 1) * lay.N + 2 * lay.N))
+
+
+def _dcgs2_close_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
+    """``_dcgs2_close`` over a lazy basis: column m becomes final (T column m = e_m)."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    h, coef = ctx.hd[: m + 1], ctx.coef
+    u = Q.col_ptr(m)
+    if tm:
+        tm.begin("block_dot")
+    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, u, h.data_ptr(), ws, tf, st)
+    if tm:
+        tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_dcgs2_coef_lazy", m, h.data_ptr(), None, h.data_ptr() + 8 * m, Hd.t.data_ptr(), Hd.k + 1,
+                coef.data_ptr(), Q.T.data_ptr(), Q.k, ws, st)
+    if tm:
+        tm.begin("block_update")
+    ctx.call("nkv_block_update", w, Q.ptr, m, coef[3 * m + 5:].data_ptr(), u, None, ws, NKV_TIME, st)
+    if tm:
+        tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
+    ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
+
+
+def _settle_basis(Q: Basis, mstart: int, lazy: bool) -> None:
+    """Before a factorisation from ``mstart``: from 1 only the caller's seed column is read, so any
+    lazy state is stale (T = I); otherwise columns < mstart must be usable — final, or (lazy run)
+    raw with the seed column mstart-1 final — else the basis is materialised first."""
+    if mstart <= 1:
+        Q.reset_T()
+    elif Q.lazy > (mstart - 1 if lazy else 0):
+        Q.materialize()
+    elif Q.lazy == 0:
+        Q.reset_T()
+
+
 def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,
                           mend: int, f: NekVector | None = None, mode: str = "cgs2", transpose: bool = False,
-                          on_step=None) -> None:
+                          on_step=None, lazy: bool = False) -> None:
     """k-step Arnoldi from column ``mstart`` to ``mend`` (1-based, inclusive), as
     krylov_decomposition.f90:68-96: f = A q_mstep; orthonormalise; Q(mstep+1) = f.
 
     ``on_step(mstep)`` is called after each step (hook for checkpointing, cf. ifres at :84); it
-    needs the finished column after every step, so with a hook ``"dcgs2"`` runs as ``"cgs2"``."""
+    needs the finished column after every step, so with a hook ``"dcgs2"`` runs as ``"cgs2"``.
+
+    ``lazy=True`` (``"dcgs2"`` only): the finished columns are left as Q = S T (see ``Basis``) —
+    one vector write less per step; on return ``Q.lazy = mend`` (column mend is final).  The
+    Krylov–Schur restart folds T into its rotation; other readers call ``Q.materialize()``."""
     if mend < mstart:
         return
     if Q.k < mend + 1:
@@ -209,11 +274,22 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     if mode == "dcgs2" and on_step is None:
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        if lazy:
+            _settle_basis(Q, mstart, lazy=True)
+            Q.mark_lazy(Q.lazy)
+            for mstep in range(mstart, mend + 1):
+                (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
+                _dcgs2_step_lazy(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
+            _dcgs2_close_lazy(ctx, Q, Hd, mend)
+            Q.mark_lazy(mend)
+            return
+        _settle_basis(Q, mstart, lazy=False)
         for mstep in range(mstart, mend + 1):
             (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
             _dcgs2_step(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
         _dcgs2_close(ctx, Q, Hd, mend)
         return
+    _settle_basis(Q, mstart, lazy=False)
     if mode == "dcgs2":
         mode = "cgs2"
     for mstep in range(mstart, mend + 1):
@@ -236,8 +312,9 @@ class FactorizationGraph:
     ``usable()`` is False for it and callers fall back to eager launches."""
 
     def __init__(self, ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, f: NekVector,
-                 mode: str = "cgs2"):
+                 mode: str = "cgs2", lazy: bool = False):
         self.ctx, self.op, self.Q, self.Hd, self.f, self.mode = ctx, op, Q, Hd, f, mode
+        self.lazy = lazy and mode == "dcgs2"
         self.graphs = {}
 
     def usable(self) -> bool:
@@ -247,14 +324,21 @@ class FactorizationGraph:
         if mend < mstart:
             return
         key = (mstart, mend, transpose)
+        Q = self.Q
+        _ = Q.T   # allocated before any capture
+        _settle_basis(Q, mstart, self.lazy)   # host-side basis state, settled outside the graph
         g = self.graphs.get(key)
         if g is None:
             timer, self.ctx.timer = self.ctx.timer, None
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.ctx.device)
+            lazy0 = Q.lazy
             with torch.cuda.graph(g):
-                arnoldi_factorization(self.ctx, self.op, self.Q, self.Hd, mstart, mend, f=self.f, mode=self.mode,
-                                      transpose=transpose)
+                arnoldi_factorization(self.ctx, self.op, Q, self.Hd, mstart, mend, f=self.f, mode=self.mode,
+                                      transpose=transpose, lazy=self.lazy)
+            Q.mark_lazy(lazy0)   # capture did not run anything
             self.ctx.timer = timer
             self.graphs[key] = g
         g.replay()
+        if self.lazy:
+            Q.mark_lazy(mend)

@@ -17,6 +17,9 @@ class KrylovSchurConfig:
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
     graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)
+    lazy_basis: bool = False       # dcgs2: leave finished columns as Q = S T (one vector write less per
+    #                                step; the restart folds T in, the result basis is materialised once;
+    #                                measured +0.3 % at N=1e8, m=128 -- DESIGN.md §6)
 
 
 @dataclass

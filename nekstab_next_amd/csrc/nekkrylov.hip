@@ -645,14 +645,48 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
 // coef layout: [x (m) | c (m+1) | rinv, y, (beta r)^2, s | a (m)].  Without hw only the pending
 // subdiagonal, the H correction, r and a are produced (closing re-orthogonalisation of the last
 // vector: q = (u - Q_m (beta a)) / (beta r)).
-__global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __restrict__ hq,
-                                                         const double* __restrict__ hw,
+//
+// Lazy basis (T != NULL): the stored columns S_0..S_{m-1} are the raw provisional vectors and the
+// orthonormal basis is Q_m = S T_m (T upper triangular, column i at T + i ldt).  The raw dots are
+// mapped first (hq <- T_m^T hq, hw <- T_m^T hw; the u entries stay), the algebra above is
+// unchanged, and instead of writing qbar the kernel appends T's column m,
+//   qbar = S_{0..m} t,  t = [-T_m a / r ; s / r],
+// and the update's coefficients z = [T_m x + t_{0:m} y ; t_m y] (coef + 3m + 5, m + 1 entries):
+// f = (A u) s/r - S_{0..m} z, one output vector.  Closing call (hw NULL): z = beta T_m a (for
+// u <- u - S_{0:m} z, then u / (beta r)) and T's column m = e_m (the closed column is final).
+__global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __restrict__ hq_raw,
+                                                         const double* __restrict__ hw_raw,
                                                          const double* __restrict__ nrm_prev,
                                                          double* __restrict__ H, int64_t ldh,
                                                          double* __restrict__ coef,
+                                                         double* __restrict__ T, int64_t ldt,
                                                          int* __restrict__ nan_flag) {
     __shared__ double lds4[4];
     __shared__ double sc[4];
+    extern __shared__ double tq[];   // lazy: [T^T hq (m+1) | T^T hw (m+1)]
+    const double* hq = hq_raw;
+    const double* hw = hw_raw;
+    if (T) {
+        double* sq = tq;
+        double* sw = tq + (m + 1);
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            const double* ti = T + (int64_t)i * ldt;
+            double a = 0.0, b = 0.0;
+            for (int l = 0; l <= i; ++l) {
+                a = fma(ti[l], hq_raw[l], a);
+                if (hw_raw) b = fma(ti[l], hw_raw[l], b);
+            }
+            sq[i] = a;
+            if (hw_raw) sw[i] = b;
+        }
+        if (threadIdx.x == 0) {
+            sq[m] = hq_raw[m];
+            if (hw_raw) sw[m] = hw_raw[m];
+        }
+        __syncthreads();
+        hq = sq;
+        hw = hw_raw ? sw : nullptr;
+    }
     const bool pend = nrm_prev != nullptr && m > 0;
     const double beta = nrm_prev ? sqrt(nrm_prev[0]) : 1.0;
     const double s1 = 1.0 / beta, s2 = s1 * s1;
@@ -713,6 +747,33 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
         coef[2 * m + 3] = r2 * beta * beta;
         coef[2 * m + 4] = s1;
         if (!(r2 > 0.0)) atomicOr(nan_flag, 1);   // breakdown: q_j in span(Q_m)
+    }
+    if (T) {   // lazy basis: T's column m and the single-output update coefficients z
+        __syncthreads();   // a (ca) and x (coef[0:m]) are written
+        double* tm = T + (int64_t)m * ldt;
+        double* z = coef + 3 * m + 5;
+        const double yv = hw ? coef[2 * m + 2] : 0.0;
+        const double tmm = s1 * rinv;
+        for (int l = threadIdx.x; l < m; l += kThreads) {
+            double ta = 0.0, tx = 0.0;
+            for (int i = l; i < m; ++i) {
+                const double t = T[(int64_t)i * ldt + l];
+                ta = fma(t, ca[i], ta);
+                if (hw) tx = fma(t, coef[i], tx);
+            }
+            if (hw) {
+                const double tl = -ta * rinv;
+                tm[l] = tl;
+                z[l] = fma(tl, yv, tx);
+            } else {
+                tm[l] = 0.0;
+                z[l] = beta * ta;
+            }
+        }
+        if (threadIdx.x == 0) {
+            tm[m] = hw ? tmm : 1.0;
+            z[m] = hw ? tmm * yv : 0.0;
+        }
     }
 }
 
@@ -891,6 +952,69 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
 #endif
     nrm = block_sum(nrm, lds4);
     if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+}
+
+// Lazy-basis DCGS2 update (see k_dcgs2_coef): f = (A u) s/r - S_{0..m} z in one read of the m+1
+// stored columns (u included), ONE output vector; the finished qbar is never written (it is
+// column m of S T).  Same tiling and streaming as the dual update.
+#ifndef NKV_DL_U
+#define NKV_DL_U 2  // columns in flight in the lazy update
+#endif
+template <int kPairs>
+__global__ __launch_bounds__(kThreads) void k_dcgs2_lazy_update(const double* __restrict__ S, int64_t ld, int m,
+                                                                const double* __restrict__ coef,
+                                                                const double* __restrict__ win,
+                                                                double* __restrict__ f, int tiles_total,
+                                                                int64_t time_off, int do_time) {
+    constexpr int kTile = kThreads * kPairs * 2;
+    constexpr int U = NKV_DL_U;
+    const double* z = coef + 3 * m + 5;
+    const double c0 = coef[2 * m + 1] * coef[2 * m + 4];   // s / r
+    const int n = m + 1;
+    if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
+        double s = 0.0;
+        for (int c = threadIdx.x; c < n; c += 64) s = fma(S[time_off + (int64_t)c * ld], z[c], s);
+        s = wave_sum(s);
+        if (threadIdx.x == 0) f[time_off] = win[time_off] * c0 - s;
+    }
+    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 af[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 fv = ld2(win + r0 + k * 2 * kThreads);
+            af[k] = make_double2(fv.x * c0, fv.y * c0);
+        }
+        const double* qb = S + r0;
+        int c = 0;
+        for (; c + U <= n; c += U) {
+            double2 q[U][kPairs];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double zc = -z[c + u];
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    af[k].x = fma(zc, q[u][k].x, af[k].x);
+                    af[k].y = fma(zc, q[u][k].y, af[k].y);
+                }
+            }
+        }
+        for (; c < n; ++c) {
+            const double zc = -z[c];
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 q = ldq(qb + (int64_t)c * ld + k * 2 * kThreads);
+                af[k].x = fma(zc, q.x, af[k].x);
+                af[k].y = fma(zc, q.y, af[k].y);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) st2s(f + r0 + k * 2 * kThreads, af[k]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1722,12 +1846,44 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
 
 int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev, double* H_dev,
                    int64_t ldh, double* coef_dev, void* ws, void* stream) {
-    if (m < 0) return fail(NKV_EINVAL, "m=%d < 0", m);
+    return nkv_dcgs2_coef_lazy(m, hq_dev, hw_dev, nrm_prev_dev, H_dev, ldh, coef_dev, nullptr, 0, ws, stream);
+}
+
+int nkv_dcgs2_coef_lazy(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev,
+                        double* H_dev, int64_t ldh, double* coef_dev, double* T_dev, int64_t ldt, void* ws,
+                        void* stream) {
+    if (m < 0 || m > NKV_MAX_COLS) return fail(NKV_EINVAL, "m=%d outside 0..%d", m, NKV_MAX_COLS);
     if (!hq_dev || !H_dev || !coef_dev) return fail(NKV_EINVAL, "hq/H/coef is NULL");
     if (ldh < m + 1) return fail(NKV_EINVAL, "ldh=%lld < m+1=%d", (long long)ldh, m + 1);
+    if (T_dev && ldt < m + 1) return fail(NKV_EINVAL, "ldt=%lld < m+1=%d", (long long)ldt, m + 1);
     CHECK(check_ptr(ws, "ws"));
-    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), 0, S(stream), m, hq_dev, hw_dev, nrm_prev_dev, H_dev,
-                       ldh, coef_dev, nan_flag_of(ws));
+    const size_t lds = T_dev ? 2 * (size_t)(m + 1) * sizeof(double) : 0;
+    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), lds, S(stream), m, hq_dev, hw_dev, nrm_prev_dev, H_dev,
+                       ldh, coef_dev, T_dev, ldt, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_dcgs2_update_lazy(const nkv_layout* L, const double* S_cols, int m, const double* coef_dev,
+                          const double* win, double* fout, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(S_cols, "S"));
+    CHECK(check_ptr(win, "win"));
+    CHECK(check_ptr(fout, "fout"));
+    if (m < 0 || m > NKV_MAX_COLS) return fail(NKV_EINVAL, "m=%d outside 0..%d", m, NKV_MAX_COLS);
+    if (!coef_dev) return fail(NKV_EINVAL, "coef is NULL");
+    (void)ws;
+    hipStream_t st = S(stream);
+    const bool large = use_large_tiles(L);
+    const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
+    const int tiles_total = (int)(rows_of(L) / (kThreads * P * 2));
+    const int gmax = NKV_DC_G < kMaxBlocks ? NKV_DC_G : kMaxBlocks;
+    int g = tiles_total < gmax ? tiles_total : gmax;
+    if (g < 1) g = 1;
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    auto kern = large ? k_dcgs2_lazy_update<NKV_DC_PAIRS> : k_dcgs2_lazy_update<NKV_PAIRS_SMALL>;
+    hipLaunchKernelGGL(kern, dim3(g), dim3(kThreads), 0, st, S_cols, L->ld, m, coef_dev, win, fout, tiles_total,
+                       rows_of(L), dt);
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -68,13 +68,16 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
     if ms > 0:
         # Only Q(1:ms) survive the restart: Q(ms+1) <- Q(k+1) below and Q(ms+2..k) are rewritten by
         # the next factorisation before any read, so the device rotation writes ms columns
-        # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.
-        Zd = torch.as_tensor(np.asfortranarray(Z[:, :ms]).ravel(order="F")).to(ctx.device)
+        # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.  A lazy basis
+        # (Q = S T, see Basis) is rotated by T Z instead: the restart materialises it for free.
+        Zr = Q.fold(np.asfortranarray(Z[:, :ms]), k)
+        Zd = torch.as_tensor(np.asfortranarray(Zr).ravel(order="F")).to(ctx.device)
         if ctx.timer:
             ctx.timer.begin("rotate")
         ctx.call("nkv_rotate_cols", Q.ptr, int(k), Zd.data_ptr(), int(k), int(ms), ctx.stream)
         if ctx.timer:
             ctx.timer.end("rotate", 8.0 * ctx.layout.N * (k + ms))
+    Q.reset_T()   # columns 0..ms-1 rotated (final); Q(k+1) is final
     H[ms, :] = b_vec @ Z
     mstart = ms + 1
     # Q(mstart) <- Q(k+1): nopcopy moves the fields only, not time (:458-459)
@@ -127,14 +130,16 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     schur_cnt = 0
     res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
     hook = None if on_step is None else (lambda mstep: on_step(mstep, Q, Hd))
-    graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode) if (cfg.graphs and hook is None) else None
+    lazy = cfg.lazy_basis and cfg.mode == "dcgs2" and hook is None
+    graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode, lazy) if (cfg.graphs and hook is None) else None
     if graphs is not None and not graphs.usable():
         graphs = None
     while True:
         if graphs is not None:
             graphs.run(mstart, k, transpose)
         else:
-            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook)
+            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook,
+                                  lazy=lazy)
         H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
         ctx.check_nan()
         vals, vecs = lapack.eig(H[:k, :k])
@@ -150,6 +155,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         Hd.upload(H)
         if on_restart is not None:
             on_restart(schur_cnt, mstart)
+    Q.materialize()   # the caller gets an orthonormal basis (one rotation per solve with a lazy basis)
     res.vals, res.vecs, res.residual, res.converged, res.schur_cnt = vals, vecs, residual, cnt, schur_cnt
     res.H = H
     return res
@@ -179,6 +185,7 @@ def orthonormality_report(ctx: NekContext, Q: Basis, k: int) -> np.ndarray:
     """Gram matrix G[i, j] = <q_i, q_j>_W (k_dot, no time term) of Q[0:k] — the self-check the
     reference writes to ``orthonormality.dat`` after the solve (eigensolvers.f90:335-345).  One
     multi-dot per column over the columns after it (upper triangle, k(k+1)/2 dots in k launches)."""
+    Q.materialize()
     G = np.zeros((k, k))
     h = ctx.h1
     for i in range(k):

@@ -234,7 +234,7 @@ def test_rotate_cols_vs_oracle(gpu, k, n_out):
         np.testing.assert_array_equal(syn.to_reference_order(lay, got[i]), Qref[i])
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2", "dcgs2-lazy"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     lay = LAYOUTS[name]
@@ -248,8 +248,13 @@ def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     Q[0].from_packed(q0)
     k_normalize(Q[0])
     Hd = HessenbergDev(ctx, m)
-    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode=mode)
+    lazy = mode == "dcgs2-lazy"
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode="dcgs2" if lazy else mode, lazy=lazy)
     H = Hd.download()
+    if lazy:   # stored columns are the raw vectors; Q = S T after materialisation
+        assert Q.lazy == m
+        Q.materialize()
+        assert Q.lazy == 0
 
     Qr = np.zeros((m + 1, L.len))
     Qr[0] = syn.to_reference_order(lay, q0)
@@ -579,7 +584,84 @@ def test_dcgs2_update_vs_numpy(gpu, name, m, with_norm):
         assert nrm.item() == -1.0   # no norm requested: nothing reduced, nothing written
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+@pytest.mark.parametrize("m", [0, 1, 5, 40])
+@pytest.mark.parametrize("with_hw", [True, False])
+@pytest.mark.parametrize("beta", [None, 1.3])
+def test_dcgs2_coef_lazy_vs_numpy(gpu, m, with_hw, beta):
+    """Lazy basis: raw dots mapped by T_m^T, then the same algebra; T gains column m
+    (t = [-T a / r ; s / r]) and z = [T x + t y ; t_m y] (closing call: z = beta T a, T col = e_m)."""
+    rng = np.random.default_rng(100 + m)
+    k = 48
+    ctx, _ = make_ctx(LAYOUTS["2d"], max_cols=k)
+    H = np.zeros((k + 1, k))
+    H[: m + 1, :m] = np.triu(rng.standard_normal((m + 1, m)), -1)
+    b_ = 1.0 if beta is None else beta
+    Tm = np.triu(1e-3 * rng.standard_normal((m, m)), 1) + np.diag(rng.uniform(0.5, 2.0, m))
+    hq_raw = np.concatenate([1e-9 * rng.standard_normal(m) * b_, [(1.0 + 1e-3) * b_ ** 2]])
+    hw_raw = rng.standard_normal(m + 1)
+    Td = torch.zeros((k, k), dtype=torch.float64, device=ctx.device)   # row c = column c of T
+    Td[:m, :m] = torch.as_tensor(Tm.T.copy())
+    Td[m, :] = 7.0   # column m is overwritten
+    Hd = HessenbergDev(ctx, k)
+    Hd.upload(H)
+    hqd = torch.as_tensor(hq_raw).to(ctx.device)
+    hwd = torch.as_tensor(hw_raw).to(ctx.device)
+    nrm = torch.tensor([b_ ** 2], dtype=torch.float64, device=ctx.device)
+    ctx.coef.zero_()
+    ctx.call_nl("nkv_dcgs2_coef_lazy", m, hqd.data_ptr(), hwd.data_ptr() if with_hw else None,
+                None if beta is None else nrm.data_ptr(), Hd.t.data_ptr(), k + 1, ctx.coef.data_ptr(),
+                Td.data_ptr(), k, ctx.ws.data_ptr(), ctx.stream)
+    hq = np.concatenate([Tm.T @ hq_raw[:m], hq_raw[m:]])
+    hw = np.concatenate([Tm.T @ hw_raw[:m], hw_raw[m:]])
+    ref = _dcgs2_coef_ref(m, hq, hw if with_hw else None, H, beta)
+    coef = ctx.coef.cpu().numpy()
+    np.testing.assert_allclose(Hd.download(), ref["H"], rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(coef[2 * m + 5: 3 * m + 5], ref["a"], rtol=1e-13, atol=1e-30)
+    Tcol = Td[m, : m + 1].cpu().numpy()
+    z = coef[3 * m + 5: 4 * m + 6]
+    if with_hw:
+        t = np.concatenate([-(Tm @ ref["a"]) * ref["rinv"], [ref["s"] * ref["rinv"]]])
+        np.testing.assert_allclose(Tcol, t, rtol=1e-12, atol=1e-20)
+        zr = np.concatenate([Tm @ ref["x"] + t[:m] * ref["y"], [t[m] * ref["y"]]])
+        np.testing.assert_allclose(z, zr, rtol=1e-12, atol=1e-14)
+    else:
+        np.testing.assert_array_equal(Tcol, np.eye(m + 1)[m])
+        np.testing.assert_allclose(z[:m], b_ * (Tm @ ref["a"]), rtol=1e-12, atol=1e-30)
+    ctx.check_nan()
+
+
+@pytest.mark.parametrize("name", list(DC_LAYOUTS))
+@pytest.mark.parametrize("m", [0, 1, 6, 31])
+def test_dcgs2_update_lazy_vs_numpy(gpu, name, m):
+    """f = (A u) s/r - S[:, 0:m+1] z: one output vector (every row incl. the time slot); the stored
+    columns are only read."""
+    lay = DC_LAYOUTS[name]
+    ctx, w = make_ctx(lay, max_cols=40)
+    Q = ctx.basis(m + 2)
+    for i in range(m + 1):
+        Q[i].fill_hash(900 + i)
+        Q[i].time = 0.05 * (i + 1)
+    f = ctx.vector()
+    f.fill_hash(78)
+    f.time = 0.4
+    rng = np.random.default_rng(m)
+    z = rng.standard_normal(m + 1) * 0.3
+    rinv, sc = 1.0 / 1.0003, 1.0 / 1.7
+    coef = np.zeros(4 * m + 8)
+    coef[2 * m + 1], coef[2 * m + 4] = rinv, sc
+    coef[3 * m + 5: 4 * m + 6] = z
+    ctx.coef[: coef.size].copy_(torch.as_tensor(coef))
+    Qh = Q.storage.cpu().numpy()
+    fh = f.to_packed()
+    ctx.call("nkv_dcgs2_update_lazy", Q.ptr, m, ctx.coef.data_ptr(), f.ptr, Q.col_ptr(m + 1), ctx.ws.data_ptr(),
+             NKV_TIME, ctx.stream)
+    fref = fh * (sc * rinv) - z @ Qh[: m + 1]
+    np.testing.assert_allclose(Q.storage[m + 1].cpu().numpy(), fref, rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(Q.storage[: m + 1].cpu().numpy(), Qh[: m + 1])
+    np.testing.assert_array_equal(f.to_packed(), fh)
+
+
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-lazy"])
 def test_arnoldi_long_vs_oracle(gpu, mode):
     """m = 300 > 256: the two-pass fallback of the fused cgs2 middle pass, DCGS2's 2j-wide dots and
     its coefficient kernel at large j, against the reference-order MGS2 oracle."""
@@ -594,8 +676,10 @@ def test_arnoldi_long_vs_oracle(gpu, mode):
     Q[0].from_packed(q0)
     k_normalize(Q[0])
     Hd = HessenbergDev(ctx, m)
-    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode=mode)
+    lazy = mode == "dcgs2-lazy"
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode="dcgs2" if lazy else mode, lazy=lazy)
     H = Hd.download()
+    Q.materialize()
     Qr = np.zeros((m + 1, L.len))
     Qr[0] = syn.to_reference_order(lay, q0)
     orc.k_normalize(L, w, Qr[0])

@@ -94,6 +94,10 @@ VARIANTS = {
     "st_sc0sc1": {"NKV_ST_AUX": 17},
     "st_ntsc1": {"NKV_ST_AUX": 18},
     "st_all": {"NKV_ST_AUX": 19},
+    "dl_u4": {"NKV_DL_U": 4},
+    "dl_u1": {"NKV_DL_U": 1},
+    "dl_g1024": {"NKV_DC_G": 1024},
+    "dl_g512": {"NKV_DC_G": 512},
 }
 
 
@@ -157,7 +161,7 @@ def run(names, E, rounds, js, only=None):
     coefs = {}
     for jj in js:   # DCGS2 coefficients for m = jj-1: small x, y, a; rinv = s = 1 (vectors stay bounded)
         mm = jj - 1
-        cj = torch.full((3 * jmax + 8,), 1e-4, dtype=torch.float64, device=dev)
+        cj = torch.full((4 * jmax + 8,), 1e-4, dtype=torch.float64, device=dev)
         cj[2 * mm + 1] = 1.0
         cj[2 * mm + 4] = 1.0
         coefs[jj] = cj
@@ -182,6 +186,9 @@ def run(names, E, rounds, js, only=None):
                                                       Q[j - 1].data_ptr(), f.data_ptr(), f2.data_ptr(), None,
                                                       ws.data_ptr(), 0x1, st),
                            8.0 * ((j - 1) * N + 4 * N)),
+            "dcgs2_lazy": (lambda: L.nkv_dcgs2_update_lazy(Lp, Q.data_ptr(), j - 1, coefs[j].data_ptr(), f.data_ptr(),
+                                                            f2.data_ptr(), ws.data_ptr(), 0x1, st),
+                           8.0 * (j * N + 2 * N)),
             "finish": (lambda: L.nkv_arnoldi_finish(Lp, f.data_ptr(), nrm1.data_ptr(), f2.data_ptr(), 0, None, None,
                                                     None, 0, st), 16.0 * N),
             "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
@@ -199,6 +206,8 @@ def run(names, E, rounds, js, only=None):
                     if only and opname not in only:
                         continue
                     if opname == "rotate_part" and not hasattr(libs[n], "nkv_rotate_cols"):
+                        continue
+                    if opname == "dcgs2_lazy" and not hasattr(libs[n], "nkv_dcgs2_update_lazy"):
                         continue
                     fn()  # warm
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
