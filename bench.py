@@ -214,6 +214,7 @@ def main():
     elapsed = comm.max_scalar(elapsed, device=dev)
     ctx.timer = None
     phases = timer.summary()
+    last_step_ms = sum(timer.last_ms(k) for k in ("block_dot2", "dcgs2_update")) if args.mode == "dcgs2" else None
     ctx.check_nan()
 
     # Krylov–Schur restart on the final factorisation (outside the timed region; reported beside
@@ -254,6 +255,20 @@ def main():
     nv_g = glay.pts_v * glay.nelgv
     value = executed_bytes(glay.N, glay.N_w, nv_g, m, args.mode, lazy) * args.steps / elapsed / 1e9
     effective = survey_model_bytes(glay.N, glay.N_w, nv_g, m) * args.steps / elapsed / 1e9
+
+    # SURVEY.md §8(d) headline: Gram–Schmidt bytes over Gram–Schmidt time only (matvec, host LAPACK
+    # and launch gaps excluded; kernel-bracketed HIP events, this rank), and the last step alone
+    gs_fams = ("block_dot", "update_dot", "block_update", "finish", "block_dot2", "dcgs2_update")
+    gs_ms = sum(phases[k]["total_ms"] for k in gs_fams if k in phases) / args.steps
+    gs_exec = sum(phases[k]["avg_bytes"] * phases[k]["launches"] for k in gs_fams if k in phases) / args.steps
+    survey_gs = survey_model_bytes(lay.N, lay.N_w, lay.n_v, m) - m * 8.0 * 3 * lay.N
+    b_last = 8.0 * (2 * m * (lay.N_w + lay.N) + 2 * (lay.N_w + lay.n_v) + 4 * lay.N + lay.n_v + 2 * lay.N)
+    gs = {"gs_ms_per_factorisation": round(gs_ms, 2),
+          "executed_gs_gbs": round(gs_exec / (gs_ms * 1e-3) / 1e9, 1),
+          "survey_headline_gbs": round(survey_gs / (gs_ms * 1e-3) / 1e9, 1),
+          "last_step_ms": None if last_step_ms is None else round(last_step_ms, 3),
+          "last_step_survey_gbs": None if last_step_ms is None else round(b_last / (last_step_ms * 1e-3) / 1e9, 1),
+          "note": "per rank; survey_* use SURVEY.md 8(d)'s 4-pass CGS2 byte model B(j) for the same work"}
 
     # Ritz accuracy vs the exact spectrum of the synthetic operator
     # (exact spectrum: the 4096 largest |mu|; a converged Ritz value is matched to the nearest one)
@@ -318,6 +333,7 @@ def main():
             },
             "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                        for k, v in phases.items()},
+            "gram_schmidt": gs,
             "ritz_rel_err": ritz_err,
             "ritz_top8_rel_err": top_err,
             "ritz_converged": int(conv.sum()),

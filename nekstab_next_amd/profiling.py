@@ -28,6 +28,12 @@ class PhaseTimer:
         ev.record(torch.cuda.current_stream(self.device))
         self.records[name].append((self._open.pop(name), ev, float(nbytes)))
 
+    def last_ms(self, name: str) -> float:
+        """Duration of the most recent launch of ``name`` (synchronises)."""
+        torch.cuda.synchronize(self.device)
+        a, b, _ = self.records[name][-1]
+        return a.elapsed_time(b)
+
     def reset(self) -> None:
         self._open.clear()
         self.records.clear()
