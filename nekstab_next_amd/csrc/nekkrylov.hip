@@ -84,6 +84,9 @@ namespace {
 #ifndef NKV_DC_SYNC
 #define NKV_DC_SYNC 0  // experiment: align the dual update's store phases over the grid (soft barrier)
 #endif
+#ifndef NKV_DC_SYNC_PCT
+#define NKV_DC_SYNC_PCT 100  // ... a block waits for this percentage of the grid (quorum)
+#endif
 #ifndef NKV_DC_SYNC_US
 #define NKV_DC_SYNC_US 20  // ... longest wait per round (us) before a block stores anyway
 #endif
@@ -896,13 +899,14 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restr
 #if NKV_DC_SYNC
         int* sync = reinterpret_cast<int*>(partials) - 16;   // the workspace's sync word (zeroed per launch)
         const int rounds = (tiles_total + gridDim.x - 1) / gridDim.x;
+        const int quorum = (int)(((int64_t)gridDim.x * NKV_DC_SYNC_PCT) / 100);
         for (int r = 0; r < rounds; ++r) {
             const int t = tile_block(blockIdx.x, gridDim.x) + r * gridDim.x;
             if (t < tiles_total)
                 dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af,
-                                   sync, (r + 1) * gridDim.x);
+                                   sync, r * gridDim.x + quorum);
             else
-                soft_barrier(sync, (r + 1) * gridDim.x);
+                soft_barrier(sync, r * gridDim.x + quorum);
         }
 #else
         for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_total; t += gridDim.x)

@@ -98,6 +98,11 @@ VARIANTS = {
     "dl_u1": {"NKV_DL_U": 1},
     "dl_g1024": {"NKV_DC_G": 1024},
     "dl_g512": {"NKV_DC_G": 512},
+    "sync_g256_q90": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256, "NKV_DC_SYNC_PCT": 90},
+    "sync_g256_q75": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256, "NKV_DC_SYNC_PCT": 75},
+    "sync_g512_q90": {"NKV_DC_SYNC": 1, "NKV_DC_G": 512, "NKV_DC_SYNC_PCT": 90},
+    "sync_g256_q90_us5": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256, "NKV_DC_SYNC_PCT": 90, "NKV_DC_SYNC_US": 5},
+    "dc_g384": {"NKV_DC_G": 384},
 }
 
 
