@@ -25,7 +25,8 @@ namespace {
 #define NKV_PAIRS 8  // double2 per thread per tile in the dot/update kernels (large problems)
 #endif
 #ifndef NKV_PAIRS_SMALL
-#define NKV_PAIRS_SMALL 2  // ... when the vector has fewer than NKV_SMALL_TILES large tiles
+#define NKV_PAIRS_SMALL 4  // ... when the vector has fewer than NKV_SMALL_TILES large tiles (4: +9-13 % on the
+                           // multi-dot at N=2e6 over 2, profiles/r01m_tune_small.log)
 #endif
 #ifndef NKV_SMALL_TILES
 #define NKV_SMALL_TILES 2048
@@ -657,6 +658,44 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
 // and the update's coefficients z = [T_m x + t_{0:m} y ; t_m y] (coef + 3m + 5, m + 1 entries):
 // f = (A u) s/r - S_{0..m} z, one output vector.  Closing call (hw NULL): z = beta T_m a (for
 // u <- u - S_{0:m} z, then u / (beta r)) and T's column m = e_m (the closed column is final).
+// out[i] = sum_{c in [lo(i), hi(i))} A(i, c) v[c] for i < m, by the whole block: row i is split
+// over P = min(8, kThreads / m) threads (strided columns, four independent accumulators, so the
+// loads of one thread are in flight together), the P partials summed in a fixed order (the result
+// does not depend on timing).  v may live in LDS or global memory; part holds max(kThreads, m)
+// doubles of LDS.  Every thread of the block must call it (it synchronises).
+template <class FA, class FLo, class FHi>
+__device__ __forceinline__ void block_matvec(int m, FA A, FLo lo, FHi hi, const double* v, double* part,
+                                             double* out) {
+    int P = m > 0 ? kThreads / m : 1;
+    P = P < 1 ? 1 : (P > 8 ? 8 : P);
+    for (int w = threadIdx.x; w < P * m; w += kThreads) {
+        const int i = w % m, q = w / m;
+        const int c1 = hi(i);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int c = lo(i) + q;
+        for (; c + 3 * P < c1; c += 4 * P) {
+            a0 = fma(A(i, c), v[c], a0);
+            a1 = fma(A(i, c + P), v[c + P], a1);
+            a2 = fma(A(i, c + 2 * P), v[c + 2 * P], a2);
+            a3 = fma(A(i, c + 3 * P), v[c + 3 * P], a3);
+        }
+        for (; c < c1; c += P) a0 = fma(A(i, c), v[c], a0);
+        part[q * m + i] = (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += kThreads) {
+        double s = 0.0;
+        for (int q = 0; q < P; ++q) s += part[q * m + i];
+        out[i] = s;
+    }
+    __syncthreads();
+}
+
+// dynamic LDS of k_dcgs2_coef (doubles): tq 2(m+1) | sa m | srow m | sg m | part max(kThreads, m)
+inline size_t dcgs2_coef_lds(int m) {
+    return (size_t)(2 * (m + 1) + 3 * m + (m > kThreads ? m : kThreads)) * sizeof(double);
+}
+
 __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __restrict__ hq_raw,
                                                          const double* __restrict__ hw_raw,
                                                          const double* __restrict__ nrm_prev,
@@ -666,42 +705,42 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
                                                          int* __restrict__ nan_flag) {
     __shared__ double lds4[4];
     __shared__ double sc[4];
-    extern __shared__ double tq[];   // lazy: [T^T hq (m+1) | T^T hw (m+1)]
+    extern __shared__ double dyn[];
+    double* tq = dyn;                 // lazy: [T^T hq (m+1) | T^T hw (m+1)]; later T x
+    double* sa = tq + 2 * (m + 1);    // a
+    double* srow = sa + m;            // H(m, c) with the pending subdiagonal filled in; later x
+    double* sg = srow + m;            // mat-vec results
+    double* part = sg + m;            // mat-vec partials
     const double* hq = hq_raw;
     const double* hw = hw_raw;
-    if (T) {
-        double* sq = tq;
-        double* sw = tq + (m + 1);
-        for (int i = threadIdx.x; i < m; i += kThreads) {
-            const double* ti = T + (int64_t)i * ldt;
-            double a = 0.0, b = 0.0;
-            for (int l = 0; l <= i; ++l) {
-                a = fma(ti[l], hq_raw[l], a);
-                if (hw_raw) b = fma(ti[l], hw_raw[l], b);
-            }
-            sq[i] = a;
-            if (hw_raw) sw[i] = b;
-        }
+    auto all = [](int) { return 0; };
+    auto to_m = [m](int) { return m; };
+    if (T) {   // hq <- T_m^T hq: (T^T h)_i = sum_{l <= i} T(l, i) h_l, column i of T contiguous
+        auto Tt = [T, ldt](int i, int l) { return T[(int64_t)i * ldt + l]; };
+        auto upto = [](int i) { return i + 1; };
+        block_matvec(m, Tt, all, upto, hq_raw, part, tq);
+        if (hw_raw) block_matvec(m, Tt, all, upto, hw_raw, part, tq + (m + 1));
         if (threadIdx.x == 0) {
-            sq[m] = hq_raw[m];
-            if (hw_raw) sw[m] = hw_raw[m];
+            tq[m] = hq_raw[m];
+            if (hw_raw) tq[2 * m + 1] = hw_raw[m];
         }
         __syncthreads();
-        hq = sq;
-        hw = hw_raw ? sw : nullptr;
+        hq = tq;
+        hw = hw_raw ? tq + (m + 1) : nullptr;
     }
     const bool pend = nrm_prev != nullptr && m > 0;
     const double beta = nrm_prev ? sqrt(nrm_prev[0]) : 1.0;
     const double s1 = 1.0 / beta, s2 = s1 * s1;
     double* ca = coef + 2 * m + 5;
-    // H(m, c) as it stands after the pending subdiagonal is filled in (c < m)
-    auto hrow = [&](int c) { return (pend && c == m - 1) ? beta : H[(int64_t)c * ldh + m]; };
     double s = 0.0, p = 0.0, tt = 0.0;
     for (int i = threadIdx.x; i < m; i += kThreads) {
         const double ai = hq[i] * s1;
+        const double hr = (pend && i == m - 1) ? beta : H[(int64_t)i * ldh + m];
+        sa[i] = ai;
         ca[i] = ai;
+        srow[i] = hr;
         s = fma(ai, ai, s);
-        tt = fma(hrow(i), ai, tt);   // t = H(m, :) a
+        tt = fma(hr, ai, tt);   // t = H(m, :) a
         if (hw) p = fma(ai, hw[i] * s1, p);
     }
     s = block_sum(s, lds4);
@@ -720,11 +759,10 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
     const double r = sqrt(r2), rinv = 1.0 / r;
     const double t = sc[2];
     if (hw) {
+        block_matvec(m, [H, ldh](int i, int c) { return H[(int64_t)c * ldh + i]; }, all, to_m, sa, part, sg);
         double* hm = H + (int64_t)m * ldh;   // column m (new, provisional)
         for (int i = threadIdx.x; i < m; i += kThreads) {
-            double ha = 0.0;
-            for (int c = 0; c < m; ++c) ha = fma(H[(int64_t)c * ldh + i], hq[c] * s1, ha);
-            const double gi = fma(hq[i] * s1, t, ha);
+            const double gi = fma(sa[i], t, sg[i]);
             const double ci = (hw[i] * s1 - gi) * rinv;
             coef[m + i] = ci;               // c_i
             coef[i] = fma(gi, rinv, ci);    // x_i
@@ -739,12 +777,16 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
         }
     }
     __syncthreads();  // every read of the old H is done before it is corrected
-    for (int c = threadIdx.x; c < m; c += kThreads) {
-        double* hc = H + (int64_t)c * ldh;
-        const double hr = hrow(c);
-        for (int i = 0; i < m; ++i) hc[i] = fma(hq[i] * s1, hr, hc[i]);
-        hc[m] = hr * r;
+    // H(0:m, c) += a H(m, c): only the columns with H(m, c) != 0 (one in a plain Arnoldi run, the
+    // restart row's columns after a Krylov–Schur condensation); the block sweeps a column at a time
+    for (int c = 0; c < m; ++c) {
+        const double hr = srow[c];
+        if (hr != 0.0) {
+            double* hc = H + (int64_t)c * ldh;
+            for (int i = threadIdx.x; i < m; i += kThreads) hc[i] = fma(sa[i], hr, hc[i]);
+        }
     }
+    for (int c = threadIdx.x; c < m; c += kThreads) H[(int64_t)c * ldh + m] = srow[c] * r;
     if (threadIdx.x == 0) {
         coef[2 * m + 1] = rinv;
         coef[2 * m + 3] = r2 * beta * beta;
@@ -752,25 +794,26 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
         if (!(r2 > 0.0)) atomicOr(nan_flag, 1);   // breakdown: q_j in span(Q_m)
     }
     if (T) {   // lazy basis: T's column m and the single-output update coefficients z
-        __syncthreads();   // a (ca) and x (coef[0:m]) are written
+        __syncthreads();   // x (coef[0:m]) and y are written; srow is free
+        for (int i = threadIdx.x; i < m; i += kThreads) srow[i] = hw ? coef[i] : 0.0;
+        __syncthreads();
+        // (T v)_l = sum_{i >= l} T(l, i) v_i
+        auto Tl = [T, ldt](int l, int i) { return T[(int64_t)i * ldt + l]; };
+        auto from = [](int l) { return l; };
+        block_matvec(m, Tl, from, to_m, sa, part, sg);              // T a
+        if (hw) block_matvec(m, Tl, from, to_m, srow, part, tq);    // T x (tq is free)
         double* tm = T + (int64_t)m * ldt;
         double* z = coef + 3 * m + 5;
         const double yv = hw ? coef[2 * m + 2] : 0.0;
         const double tmm = s1 * rinv;
         for (int l = threadIdx.x; l < m; l += kThreads) {
-            double ta = 0.0, tx = 0.0;
-            for (int i = l; i < m; ++i) {
-                const double t = T[(int64_t)i * ldt + l];
-                ta = fma(t, ca[i], ta);
-                if (hw) tx = fma(t, coef[i], tx);
-            }
             if (hw) {
-                const double tl = -ta * rinv;
+                const double tl = -sg[l] * rinv;
                 tm[l] = tl;
-                z[l] = fma(tl, yv, tx);
+                z[l] = fma(tl, yv, tq[l]);
             } else {
                 tm[l] = 0.0;
-                z[l] = beta * ta;
+                z[l] = beta * sg[l];
             }
         }
         if (threadIdx.x == 0) {
@@ -1824,7 +1867,9 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     // large problems: one block row walks every field of its tiles (weights read once per tile)
     const int nf = (large && NKV_D2_FIELDLOOP) ? L->n_wf : 1;
     const int gy = L->n_wf / nf;
-    int bx = (NKV_D2_MAXB < kMaxBlocks ? NKV_D2_MAXB : kMaxBlocks) / gy;
+    // one workgroup per CU for large problems (8 rows/thread keep enough loads in flight); small
+    // problems (2 rows/thread) need the full kMaxBlocks grid to fill the chip
+    int bx = (large ? (NKV_D2_MAXB < kMaxBlocks ? NKV_D2_MAXB : kMaxBlocks) : kMaxBlocks) / gy;
     if (bx > tpf) bx = tpf;
     if (bx < 1) bx = 1;
     const int B = bx * gy;
@@ -1861,8 +1906,8 @@ int nkv_dcgs2_coef_lazy(int m, const double* hq_dev, const double* hw_dev, const
     if (ldh < m + 1) return fail(NKV_EINVAL, "ldh=%lld < m+1=%d", (long long)ldh, m + 1);
     if (T_dev && ldt < m + 1) return fail(NKV_EINVAL, "ldt=%lld < m+1=%d", (long long)ldt, m + 1);
     CHECK(check_ptr(ws, "ws"));
-    const size_t lds = T_dev ? 2 * (size_t)(m + 1) * sizeof(double) : 0;
-    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), lds, S(stream), m, hq_dev, hw_dev, nrm_prev_dev, H_dev,
+    hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), dcgs2_coef_lds(m), S(stream), m, hq_dev, hw_dev,
+                       nrm_prev_dev, H_dev,
                        ldh, coef_dev, T_dev, ldt, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;

@@ -103,6 +103,10 @@ VARIANTS = {
     "sync_g512_q90": {"NKV_DC_SYNC": 1, "NKV_DC_G": 512, "NKV_DC_SYNC_PCT": 90},
     "sync_g256_q90_us5": {"NKV_DC_SYNC": 1, "NKV_DC_G": 256, "NKV_DC_SYNC_PCT": 90, "NKV_DC_SYNC_US": 5},
     "dc_g384": {"NKV_DC_G": 384},
+    "ps4": {"NKV_PAIRS_SMALL": 4},
+    "ps1": {"NKV_PAIRS_SMALL": 1},
+    "d2u4": {"NKV_D2_U": 4},
+    "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
 }
 
 
