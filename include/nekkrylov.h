@@ -56,6 +56,9 @@ extern "C" {
  * live in LDS (64 B per column for the two-vector dot).  The reference's k_dim defaults to 100
  * (main.f90:9); GMRES on the cylinder uses 200 (1cyl.usr:14). */
 #define NKV_MAX_COLS 1024
+/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols): the Krylov–Schur
+ * restart and the materialisation of a lazy DCGS2 basis, so k_dim <= 576 for both. */
+#define NKV_ROT_MAX_K 576
 
 /* Status codes (every entry point). */
 #define NKV_OK 0

@@ -35,6 +35,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import _lib
 from ._lib import NKV_NORM2, NKV_TIME, NKV_TIME_DOT, NKV_X_IS_LAST
 from .operators import LinearOperator
 from .vector import Basis, NekContext, NekVector
@@ -274,6 +275,8 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     if mode == "dcgs2" and on_step is None:
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        if lazy and mend > _lib.NKV_ROT_MAX_K:   # a lazy basis this wide could not be materialised
+            lazy = False
         if lazy:
             _settle_basis(Q, mstart, lazy=True)
             Q.mark_lazy(Q.lazy)
@@ -325,8 +328,9 @@ class FactorizationGraph:
             return
         key = (mstart, mend, transpose)
         Q = self.Q
+        lazy = self.lazy and mend <= _lib.NKV_ROT_MAX_K
         _ = Q.T   # allocated before any capture
-        _settle_basis(Q, mstart, self.lazy)   # host-side basis state, settled outside the graph
+        _settle_basis(Q, mstart, lazy)   # host-side basis state, settled outside the graph
         g = self.graphs.get(key)
         if g is None:
             timer, self.ctx.timer = self.ctx.timer, None
@@ -335,10 +339,10 @@ class FactorizationGraph:
             lazy0 = Q.lazy
             with torch.cuda.graph(g):
                 arnoldi_factorization(self.ctx, self.op, Q, self.Hd, mstart, mend, f=self.f, mode=self.mode,
-                                      transpose=transpose, lazy=self.lazy)
+                                      transpose=transpose, lazy=lazy)
             Q.mark_lazy(lazy0)   # capture did not run anything
             self.ctx.timer = timer
             self.graphs[key] = g
         g.replay()
-        if self.lazy:
+        if lazy:
             Q.mark_lazy(mend)

@@ -107,7 +107,7 @@ static_assert(NKV_TILE % (kThreads * NKV_PAIRS_SMALL * 2) == 0, "kernel tile mus
 constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots per column
 constexpr int kColUnroll = NKV_COLU;                 // columns in flight per thread (block dot)
 constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
-constexpr int kRotMaxK = 576;                        // rotation: 64-row tiles up to k=256, 32-row beyond
+constexpr int kRotMaxK = NKV_ROT_MAX_K;               // rotation: 64-row tiles up to k=256, 32-row beyond
 
 // Tile order of a grid-stride loop.  Blocks b and b+8 share an XCD (round-robin dispatch,
 // MI355X_MICROARCH.md §Workgroup dispatch); with NKV_XCD_MAP the G/8 blocks of one XCD take

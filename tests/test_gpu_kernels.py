@@ -725,3 +725,47 @@ def test_fortran_host_example_runs(gpu):
     p = subprocess.run([exe, "512", "24"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "arnoldi_f: OK" in p.stdout
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "dcgs2-lazy"])
+def test_arnoldi_at_max_columns(gpu, mode):
+    """m = 1000 steps, max_cols = 1001: the widest factorisation the ABI takes (NKV_MAX_COLS = 1024
+    bounds the closing multi-dot; the two-vector dot keeps 8j partials in LDS, the coefficient
+    kernel its j-vectors).  The lazy basis falls back to eager columns above NKV_ROT_MAX_K.  Checks:
+    W-orthonormality of all 1001 columns, the Arnoldi relation, and the first 20 columns of H
+    against the reference-order oracle."""
+    from nekstab_next_amd import _lib
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=60)   # N_w = 4,320 > m
+    m = 1000
+    ctx, w = make_ctx(lay, max_cols=m + 1)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    Q = ctx.basis(m + 1)
+    q0 = syn.hash_vector(lay, 5)
+    Q[0].from_packed(q0)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, m)
+    lazy = mode == "dcgs2-lazy"
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode="dcgs2" if lazy else mode, lazy=lazy)
+    assert Q.lazy == 0 and m > _lib.NKV_ROT_MAX_K
+    ctx.check_nan()
+    H = Hd.download()
+    Qh = Q.storage.cpu().numpy()
+    wf = _wfull(lay, w)
+    G = Qh @ (wf[None, :] * Qh).T
+    assert np.max(np.abs(G - np.eye(m + 1))) < 1e-12
+    f = ctx.vector()
+    for jcol in (0, 499, m - 1):   # A q_j - Q[:, :j+2] H[:j+2, j]
+        op.matvec(Q[jcol], f)
+        r = f.to_packed() - H[: jcol + 2, jcol] @ Qh[: jcol + 2]
+        assert np.sqrt(np.sum(wf * r * r)) <= 1e-12 * np.max(np.abs(H)), jcol
+    L = olayout(lay)
+    Qr = np.zeros((21, L.len))
+    Qr[0] = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, Qr[0])
+    Hr = np.zeros((21, 20))
+    dref = syn.to_reference_order(lay, d)
+    orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.0),
+                              Qr, Hr, 1, 20)
+    assert np.max(np.abs(H[:21, :20] - Hr)) <= 1e-12 * np.max(np.abs(Hr))
