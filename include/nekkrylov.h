@@ -56,8 +56,9 @@ extern "C" {
  * live in LDS (64 B per column for the two-vector dot).  The reference's k_dim defaults to 100
  * (main.f90:9); GMRES on the cylinder uses 200 (1cyl.usr:14). */
 #define NKV_MAX_COLS 1024
-/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols): the Krylov–Schur
- * restart and the materialisation of a lazy DCGS2 basis, so k_dim <= 576 for both. */
+/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols with more than 8 output
+ * columns): a Krylov–Schur restart keeping more than 8 vectors and the materialisation of a lazy
+ * DCGS2 basis, so those need k_dim <= 576. */
 #define NKV_ROT_MAX_K 576
 
 /* Status codes (every entry point). */
@@ -192,7 +193,8 @@ int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int l
 /* Partial restart rotation, in place: Q[:,0:n_out] <- Q[:,0:k] * V[:,0:n_out], 1 <= n_out <= k.
  * Columns n_out..k-1 are left as they were.  schur_condensation only keeps the mstart selected
  * Schur vectors (eigensolvers.f90:416-459: Q(mstart+1..k) are overwritten by the next
- * factorisation before being read), so the restart calls this with n_out = mstart. */
+ * factorisation before being read), so the restart calls this with n_out = mstart.
+ * k <= NKV_ROT_MAX_K, or k <= NKV_MAX_COLS when n_out <= 8 (the usual restart). */
 int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out,
                     void* stream);
 

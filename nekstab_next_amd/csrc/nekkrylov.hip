@@ -2099,7 +2099,9 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
     CHECK(check_layout(L));
     CHECK(check_ptr(Q, "Q"));
     if (!V_dev) return fail(NKV_EINVAL, "V_dev is NULL");
-    if (k < 1 || k > kRotMaxK) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d]", k, kRotMaxK);
+    // the few-column streaming kernel holds no k-sized state: any k up to NKV_MAX_COLS
+    const int kmax = (n_out >= 1 && n_out <= NKV_ROTF_MAX) ? NKV_MAX_COLS : kRotMaxK;
+    if (k < 1 || k > kmax) return fail(NKV_EINVAL, "rotate: k=%d outside [1, %d] (n_out=%d)", k, kmax, n_out);
     if (ldv < k) return fail(NKV_EINVAL, "rotate: ldv=%d < k=%d", ldv, k);
     if (n_out < 1 || n_out > k) return fail(NKV_EINVAL, "rotate: n_out=%d outside [1, k=%d]", n_out, k);
     if (NKV_ROT_VALU && n_out == k) return rotate_valu(L, Q, k, V_dev, ldv, stream);
