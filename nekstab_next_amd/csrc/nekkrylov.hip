@@ -200,6 +200,36 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+#ifndef NKV_D2_RED
+#define NKV_D2_RED 1  // transposed wave reduction in the multi-dots (DPP within rows): +4-10 % on
+                      // the two-vector dot at N=2e6, +0.3 % at N=1e8 (profiles/r01m_tune_d2red.log)
+#endif
+
+// One DPP move of a double (two 32-bit halves), every lane reading its source lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(__double_as_longlong(v) & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(__double_as_longlong(v) >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sums of FOUR per-lane values over the 64 lanes in 7 exchanges instead of 24: the xor-32 and
+// xor-16 steps each hand half of the values to the partner (so every lane keeps one value from
+// there on), the in-row steps run on DPP (quad xor 1, quad xor 2, half-row mirror, row mirror).
+// Value v lands in lane 16 v (v = 0..3).  Deterministic (a fixed exchange pattern).
+__device__ __forceinline__ double wave_sum4(double s0, double s1, double s2, double s3, int lane) {
+    const bool up = (lane & 32) != 0;
+    const double k0 = (up ? s2 : s0) + __shfl_xor(up ? s0 : s2, 32, 64);
+    const double k1 = (up ? s3 : s1) + __shfl_xor(up ? s1 : s3, 32, 64);
+    const bool b4 = (lane & 16) != 0;
+    double v = (b4 ? k1 : k0) + __shfl_xor(b4 ? k0 : k1, 16, 64);
+    v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);   // row_half_mirror
+    v += dpp_d<0x140>(v);   // row_mirror
+    return v;
+}
+
 // Block-wide sum of one double (256 threads); result valid in thread 0.
 __device__ __forceinline__ double block_sum(double v, double* lds4) {
     v = wave_sum(v);
@@ -299,6 +329,10 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
                 }
                 s[u] = a;
             }
+#if NKV_D2_RED && NKV_COLU == 4   // four columns = four sums
+            const double v = wave_sum4(s[0], s[1], s[2], s[3], lane);
+            if ((lane & 15) == 0) red[wave * j + c + (lane >> 4)] += v;
+#else
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
@@ -307,6 +341,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
 #pragma unroll
                 for (int u = 0; u < kColUnroll; ++u) red[wave * j + c + u] += s[u];
             }
+#endif
         }
         for (; c < j; ++c) {
             double a = 0.0;
@@ -609,6 +644,14 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                     s[u] = a;
                     s[U + u] = b;
                 }
+#if NKV_D2_RED && NKV_D2_U == 2   // two columns x two right-hand sides = four sums
+                const double v = wave_sum4(s[0], s[1], s[2], s[3], lane);
+                if ((lane & 15) == 0) {
+                    const int q = lane >> 4;                 // 0: x.c  1: x.(c+1)  2: y.c  3: y.(c+1)
+                    const int cc = c + (q & 1);
+                    if (cc < jl) red[wave * 2 * j + (q >> 1) * j + cc] += v;
+                }
+#else
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
@@ -622,6 +665,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                         }
                     }
                 }
+#endif
             }
         }
     }

@@ -107,6 +107,7 @@ VARIANTS = {
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
+    "d2red": {"NKV_D2_RED": 1},
 }
 
 
