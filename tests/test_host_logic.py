@@ -95,3 +95,29 @@ def test_schur_ordschur_lstsq():
     b = rng.standard_normal(n + 1)
     np.testing.assert_allclose(lapack.lstsq(B, b), np.linalg.lstsq(B, b, rcond=None)[0], rtol=1e-10)
     np.testing.assert_array_equal(lapack.lstsq(B, b), orc.lstsq(B, b))
+
+
+def test_lazy_basis_fold_is_T_times_y():
+    """Basis.fold (lazy DCGS2 basis Q = S T): combinations of the first k final columns become
+    combinations of the stored columns with coefficients T y on the first ``lazy`` entries; host
+    arrays and tensors alike (the device tensor is replaced by a CPU one here)."""
+    import torch
+
+    from nekstab_next_amd.vector import Basis
+
+    rng = np.random.default_rng(3)
+    k, L = 9, 6
+    T = np.triu(rng.standard_normal((k, k)))
+    B = object.__new__(Basis)
+    B.k, B.lazy, B._T_identity = k, L, False
+    B._T = torch.as_tensor(T.T.copy())   # row c = column c of T
+    y = rng.standard_normal(k)
+    want = y.copy()
+    want[:L] = T[:L, :L] @ y[:L]
+    np.testing.assert_allclose(B.fold(y, k), want, rtol=1e-15)
+    np.testing.assert_allclose(B.fold(torch.as_tensor(y), k).numpy(), want, rtol=1e-15)
+    Z = rng.standard_normal((k, 3))       # a restart's V: every column folded
+    np.testing.assert_allclose(B.fold(Z, k)[:L], T[:L, :L] @ Z[:L], rtol=1e-14)
+    np.testing.assert_array_equal(B.fold(Z, k)[L:], Z[L:])
+    B.lazy = 0
+    assert B.fold(y, k) is y
