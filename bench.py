@@ -343,6 +343,11 @@ def main():
             "restart": restart,
         }
         print(json.dumps(out), flush=True)
+    comm.barrier()
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()   # every rank leaves the RCCL group before the process exits
 
 
 if __name__ == "__main__":
