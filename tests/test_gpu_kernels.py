@@ -769,3 +769,77 @@ def test_arnoldi_at_max_columns(gpu, mode):
     orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.0),
                               Qr, Hr, 1, 20)
     assert np.max(np.abs(H[:21, :20] - Hr)) <= 1e-12 * np.max(np.abs(Hr))
+
+
+def test_legacy_krylov_vector_api_vs_oracle(gpu):
+    """The free-subroutine krylov_vector API (krylov_subspace.f90:94-161) over the device vectors —
+    k_zero, k_copy (fields and time), k_cmult, k_add2, k_sub2, k_sub3 — against the oracle's C
+    restatement on the same data, every op carrying the time slot."""
+    from nekstab_next_amd.vector import k_add2, k_cmult, k_copy, k_sub2, k_sub3, k_zero
+
+    lay = LAYOUTS["3d_scalar"]
+    ctx, _ = make_ctx(lay)
+    L = olayout(lay)
+    c = ctypes.byref(L.c)
+    a, b = syn.hash_vector(lay, 41), syn.hash_vector(lay, 42)
+    a[lay.time_offset], b[lay.time_offset] = 0.75, -0.5
+    p, q, r = dev_vec(ctx, a), dev_vec(ctx, b), ctx.vector()
+    rp, rq, rr = syn.to_reference_order(lay, a), syn.to_reference_order(lay, b), np.zeros(L.len)
+
+    def same(v, ref):
+        np.testing.assert_array_equal(syn.to_reference_order(lay, v.to_packed()), ref)
+
+    k_copy(r, p)
+    orc.lib().orc_k_copy(c, rr, rp)
+    same(r, rr)
+    assert r.time == 0.75
+    k_cmult(r, 1.5)
+    orc.lib().orc_k_cmult(c, rr, 1.5)
+    same(r, rr)
+    k_add2(r, q)
+    orc.lib().orc_k_add2(c, rr, rq)
+    same(r, rr)
+    k_sub2(r, p)
+    orc.lib().orc_k_sub2(c, rr, rp)
+    same(r, rr)
+    k_sub3(r, q, p)
+    orc.lib().orc_k_sub3(c, rr, rq, rp)
+    same(r, rr)
+    k_zero(r)
+    orc.lib().orc_k_zero(c, rr)
+    same(r, rr)
+    assert r.time == 0.0
+
+
+@pytest.mark.parametrize("k,tgt", [(16, 5), (24, 2), (40, 4)])
+def test_schur_condensation_vs_oracle(gpu, k, tgt):
+    """One Krylov–Schur restart (eigensolvers.f90:363-468) on the same factorisation: mstart and the
+    selected set identical, the condensed H (Schur block, bᵀZ row) and the rotated kept columns
+    plus the moved last vector to 1e-12."""
+    from nekstab_next_amd.krylov_schur import schur_condensation
+
+    lay = LAYOUTS["2d"]
+    ctx, w = make_ctx(lay, max_cols=48)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    Q = ctx.basis(k + 1)
+    q0 = syn.hash_vector(lay, 9)
+    Q[0].from_packed(q0)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, k)
+    arnoldi_factorization(ctx, op, Q, Hd, 1, k, mode="dcgs2")
+    H = np.array(Hd.download(), order="F")
+    Qh = Q.storage.cpu().numpy()
+    Qr = np.array([syn.to_reference_order(lay, Qh[i]) for i in range(k + 1)])
+    Hr = H.copy(order="F")
+    from nekstab_next_amd.config import KrylovSchurConfig
+    ms_d, sel_d = schur_condensation(ctx, H, Q, k, KrylovSchurConfig(k_dim=k, schur_tgt=tgt))
+    ms_r, sel_r = orc.schur_condensation(L, Hr, Qr, k, 0.1, tgt)
+    assert ms_d == ms_r
+    np.testing.assert_array_equal(sel_d, sel_r)
+    np.testing.assert_allclose(H, Hr, rtol=0, atol=1e-12 * np.max(np.abs(Hr)))
+    got = Q.storage.cpu().numpy()
+    for i in list(range(ms_d - 1)) + [ms_d - 1]:   # kept Schur vectors and Q(mstart) <- Q(k+1)
+        gi = syn.to_reference_order(lay, got[i])
+        np.testing.assert_allclose(gi[: L.n], Qr[i, : L.n], rtol=0, atol=1e-12)

@@ -121,3 +121,18 @@ def test_lazy_basis_fold_is_T_times_y():
     np.testing.assert_array_equal(B.fold(Z, k)[L:], Z[L:])
     B.lazy = 0
     assert B.fold(y, k) is y
+
+
+@pytest.mark.parametrize("n", [2, 5, 16, 64, 128])
+def test_sort_eigendecomp_python_equals_c(n):
+    """sort_eigendecomp (lapack_wrapper.f90:181-228): exchange sort by |lambda|, strict <, columns
+    of the eigenvector matrix moved with their values — product vs the oracle's C, bit for bit,
+    conjugate pairs (equal moduli) keeping LAPACK's order."""
+    rng = np.random.default_rng(n)
+    for _ in range(10):
+        vals = _spectrum(rng, n, ties=True)
+        vecs = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        v1, e1 = lapack.sort_eigendecomp(vals.copy(), vecs.copy())
+        v2, e2 = orc.sort_eigendecomp(vals.copy(), vecs.copy())
+        np.testing.assert_array_equal(v1, v2)
+        np.testing.assert_array_equal(e1, e2)

@@ -196,6 +196,10 @@ def run(names, E, rounds, js, only=None):
                                                       Q[j - 1].data_ptr(), f.data_ptr(), f2.data_ptr(), None,
                                                       ws.data_ptr(), 0x1, st),
                            8.0 * ((j - 1) * N + 4 * N)),
+            "dcgs2_inpl": (lambda: L.nkv_dcgs2_update(Lp, w.data_ptr(), Q.data_ptr(), j - 1, coefs[j].data_ptr(),
+                                                      Q[j - 1].data_ptr(), f2.data_ptr(), f2.data_ptr(), None,
+                                                      ws.data_ptr(), 0x1, st),
+                           8.0 * ((j - 1) * N + 4 * N)),
             "dcgs2_lazy": (lambda: L.nkv_dcgs2_update_lazy(Lp, Q.data_ptr(), j - 1, coefs[j].data_ptr(), f.data_ptr(),
                                                             f2.data_ptr(), ws.data_ptr(), 0x1, st),
                            8.0 * (j * N + 2 * N)),
