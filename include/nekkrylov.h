@@ -142,6 +142,25 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
                        int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
                        unsigned flags, void* stream);
 
+/* The remaining block entry points SURVEY.md §8(b) names:
+ * nkv_combine:          out <- Q[:,0:k] y  (k_matmul krylov_subspace.f90:163-209, mode
+ *                       reconstruction eigensolvers.f90:565-585; = nkv_block_update NKV_OVERWRITE)
+ * nkv_normalize_store:  q_next <- f / sqrt(*nrm2_dev), *beta_dev = sqrt(*nrm2_dev) (the reduced
+ *                       ||f||_W^2; update_hessenberg_matrix's last lines :183-186 with Q(k+1) = f, :81)
+ * nkv_mgs2_step:        the reference's whole update_hessenberg_matrix in ITS operation order
+ *                       (:155-186: two MGS passes, one weighted dot + axpy per column, H(i,k) =
+ *                       alpha1 + alpha2, H(k+1,k) = ||f||, q_out = f/||f||), device-side with no
+ *                       host sync.  SINGLE PROCESS: its dots are not all-reduced — a sharded host
+ *                       runs nkv_dot + all-reduce + nkv_axpy_dev per column (the mgs2 mode of
+ *                       nekstab_next_amd.arnoldi).  hcol_dev: j+1 doubles.  NKV_TIME_DOT adds the
+ *                       time products to the dots (uparam(1)==2.1, rank0); f.time follows the axpys. */
+int nkv_combine(const nkv_layout* L, const double* Q, int k, const double* y_dev, double* out, unsigned flags,
+                void* stream);
+int nkv_normalize_store(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_next,
+                        double* beta_dev, unsigned flags, void* stream);
+int nkv_mgs2_step(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
+                  double* hcol_dev, void* ws, unsigned flags, void* stream);
+
 /* ---- DCGS2: classical Gram–Schmidt with delayed re-orthogonalisation (two reads of Q per step,
  * ONE all-reduce per step, no separate normalisation pass).  Same replacement target as the CGS2
  * entry points above (update_hessenberg_matrix, krylov_decomposition.f90:103-189); the

@@ -2038,6 +2038,63 @@ int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_
     return NKV_OK;
 }
 
+int nkv_combine(const nkv_layout* L, const double* Q, int k, const double* y_dev, double* out, unsigned flags,
+                void* stream) {
+    return nkv_block_update(L, nullptr, Q, k, y_dev, out, nullptr, nullptr,
+                            (flags & ~(unsigned)NKV_NORM2) | NKV_OVERWRITE, stream);
+}
+
+int nkv_normalize_store(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_next,
+                        double* beta_dev, unsigned flags, void* stream) {
+    (void)flags;
+    CHECK(check_layout(L));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(q_next, "q_next"));
+    if (!nrm2_dev) return fail(NKV_EINVAL, "nrm2_dev is NULL");
+    const int64_t rows = rows_of(L);
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(rows / 2)), dim3(kThreads), 0, S(stream), f, nrm2_dev, q_next, rows,
+                       rows, 0, nullptr, nullptr, nullptr, beta_dev);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+__global__ void k_accumulate(double* __restrict__ dst, const double* __restrict__ src) {
+    if (threadIdx.x == 0) dst[0] += src[0];
+}
+
+int nkv_mgs2_step(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
+                  double* hcol_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(q_out, "q_out"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!hcol_dev) return fail(NKV_EINVAL, "hcol_dev is NULL");
+    if (j < 0 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 0..%d", j, NKV_MAX_COLS);
+    if (j > 0) CHECK(check_ptr(Q, "Q"));
+    const unsigned tdot = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+    double* tmp = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 128);   // control-area scratch
+    hipStream_t st = S(stream);
+    for (int pass = 0; pass < 2; ++pass) {   // krylov_decomposition.f90:155-168, then :171-180
+        for (int i = 0; i < j; ++i) {
+            const double* qi = Q + (int64_t)i * L->ld;
+            double* h = pass == 0 ? hcol_dev + i : tmp;
+            CHECK(nkv_dot(L, w, f, qi, h, ws, tdot, st));                   // alpha = <f, q_i>
+            CHECK(nkv_axpy_dev(L, f, h, -1.0, qi, NKV_TIME, st));           // f <- f - alpha q_i
+            if (pass == 1) {
+                hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, st, hcol_dev + i, tmp);   // H(i,k) += alpha2
+                NKV_LAUNCHED();
+            }
+        }
+    }
+    CHECK(nkv_dot(L, w, f, f, tmp + 1, ws, tdot, st));                       // ||f||^2
+    const int64_t rows = rows_of(L);                                          // q_out = f/||f||, H(k+1,k)
+    hipLaunchKernelGGL(k_finish, dim3(grid_for(rows / 2)), dim3(kThreads), 0, st, f, tmp + 1, q_out, rows, rows, 0,
+                       nullptr, nullptr, nullptr, hcol_dev + j);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
 #ifndef NKV_ROT_VALU
 #define NKV_ROT_VALU 0   // 1: the VALU (4x4 register block) rotation instead of the f64 MFMA one
 #endif

@@ -843,3 +843,57 @@ def test_schur_condensation_vs_oracle(gpu, k, tgt):
     for i in list(range(ms_d - 1)) + [ms_d - 1]:   # kept Schur vectors and Q(mstart) <- Q(k+1)
         gi = syn.to_reference_order(lay, got[i])
         np.testing.assert_allclose(gi[: L.n], Qr[i, : L.n], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("time_dot", [False, True])
+def test_mgs2_step_combine_normalize_store_vs_oracle(gpu, time_dot):
+    """SURVEY §8(b)'s remaining entry points: nkv_mgs2_step (the whole update_hessenberg_matrix in
+    the reference's operation order, one process) against the oracle's update_hessenberg on the same
+    basis and f — H column to 1e-13·max, q_out to 1e-13; nkv_combine = Q y; nkv_normalize_store =
+    f/||f|| with beta returned."""
+    from nekstab_next_amd._lib import NKV_TIME, NKV_TIME_DOT
+
+    lay = LAYOUTS["3d_scalar"]
+    ctx, w = make_ctx(lay, max_cols=16)
+    L = olayout(lay, time_in_dot=time_dot)
+    d, _ = syn.diag_spectrum(lay)
+    dref = syn.to_reference_order(lay, d)
+    j = 7
+    Qr = np.zeros((j + 1, L.len))
+    Qr[0] = syn.to_reference_order(lay, syn.hash_vector(lay, 21))
+    Qr[0, -1] = 0.3 if time_dot else 0.0
+    orc.k_normalize(L, w, Qr[0])
+    Hr = np.zeros((j + 1, j))
+    mv = lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.5)  # noqa: E731
+    orc.arnoldi_factorization(L, w, mv, Qr, Hr, 1, j - 1)    # Q[0:j] orthonormal
+    f_ref = np.zeros(L.len)
+    mv(Qr[j - 1], f_ref)
+    Q = ctx.basis(j + 1)
+    for i in range(j):
+        Q[i].from_packed(syn.from_reference_order(lay, Qr[i]))
+    f = ctx.vector().from_packed(syn.from_reference_order(lay, f_ref))
+    hcol = torch.zeros(j + 1, dtype=torch.float64, device=ctx.device)
+    q_out = ctx.vector()
+    ctx.call("nkv_mgs2_step", ctx.w.data_ptr(), Q.ptr, j, f.ptr, q_out.ptr, hcol.data_ptr(), ctx.ws.data_ptr(),
+             NKV_TIME_DOT if time_dot else 0, ctx.stream)
+    col = np.zeros(j + 1)
+    wrk = L.zeros()
+    fr = f_ref.copy()
+    orc.lib().orc_update_hessenberg(ctypes.byref(L.c), w, col, fr, np.ascontiguousarray(Qr[:j]), j, wrk)
+    h = hcol.cpu().numpy()
+    np.testing.assert_allclose(h, col, rtol=0, atol=1e-13 * np.max(np.abs(col)))
+    np.testing.assert_allclose(syn.to_reference_order(lay, q_out.to_packed()), fr, rtol=0, atol=1e-13)
+    # nkv_combine: out = Q[:, :j] y (fields and time)
+    y = np.random.default_rng(1).standard_normal(j)
+    yd = torch.as_tensor(y).to(ctx.device)
+    out = ctx.vector()
+    ctx.call("nkv_combine", Q.ptr, j, yd.data_ptr(), out.ptr, NKV_TIME, ctx.stream)
+    want = y @ Q.storage[:j].cpu().numpy()
+    np.testing.assert_allclose(out.to_packed(), want, rtol=1e-13, atol=1e-14)
+    # nkv_normalize_store: q_next = f / sqrt(nrm2), beta returned
+    nrm2 = torch.tensor([4.0], dtype=torch.float64, device=ctx.device)
+    beta = torch.zeros(1, dtype=torch.float64, device=ctx.device)
+    qn = ctx.vector()
+    ctx.call("nkv_normalize_store", out.ptr, nrm2.data_ptr(), qn.ptr, beta.data_ptr(), 0, ctx.stream)
+    np.testing.assert_array_equal(qn.to_packed(), out.to_packed() * 0.5)
+    assert beta.item() == 2.0
