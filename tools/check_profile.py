@@ -2,10 +2,12 @@
 """Compare rocprofv3 --stats per-kernel-family average durations with bench.py's live HIP-event
 phase timings (the bench's `roofline.avg_launch_ms` must agree with the profiler).
 
-usage: tools/check_profile.py KERNEL_STATS_CSV BENCH_JSON
+usage: tools/check_profile.py KERNEL_STATS_CSV BENCH_JSON   (run_kernel_trace.csv beside the stats
+       file, when present, gives the per-launch comparison for families with unbracketed launches)
 """
 import csv
 import json
+import os
 import sys
 
 FAM = {"block_dot": "k_block_dot<", "block_dot2": "k_block_dot2<", "dcgs2_update": "k_dcgs2_update<",
@@ -16,6 +18,8 @@ FAM = {"block_dot": "k_block_dot<", "block_dot2": "k_block_dot2<", "dcgs2_update
 def main():
     stats = list(csv.DictReader(open(sys.argv[1])))
     bench = json.load(open(sys.argv[2]))
+    tpath = os.path.join(os.path.dirname(sys.argv[1]), "run_kernel_trace.csv")
+    trace = list(csv.DictReader(open(tpath))) if os.path.exists(tpath) else None
     print(f"{'family':14s} {'rocprof calls':>13s} {'rocprof avg ms':>15s} {'events launches':>16s} {'events avg ms':>14s} {'ratio':>7s}")
     for fam, key in FAM.items():
         rows = [r for r in stats if key in r["Name"]]
@@ -26,6 +30,16 @@ def main():
         ph = bench.get("phases", {}).get(fam)
         ev = f"{ph['launches']:16d} {ph['avg_ms']:14.4f} {ph['avg_ms'] / (tot / calls / 1e6):7.3f}" if ph else ""
         print(f"{fam:14s} {calls:13d} {tot / calls / 1e6:15.4f} {ev}")
+        if ph and trace and abs(ph["avg_ms"] / (tot / calls / 1e6) - 1.0) > 0.05:
+            # the family also runs outside the bracketed launches (block_dot: the j=1 seed dot of
+            # every step besides the bracketed closing dot): compare the bracketed ones, i.e. the
+            # `launches` longest launches of the trace
+            durs = sorted(((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace
+                           if key in r["Kernel_Name"]), reverse=True)[: ph["launches"]]
+            if durs:
+                avg = sum(durs) / len(durs)
+                print(f"{'  (longest)':14s} {len(durs):13d} {avg:15.4f} {ph['launches']:16d} {ph['avg_ms']:14.4f} "
+                      f"{ph['avg_ms'] / avg:7.3f}")
     print("(rocprof counts every launch incl. warm-up and the j=1 seed dots; events cover the timed steps; "
           "event brackets include the ~5 us second-stage reduction kernel)")
     rs = bench.get("restart")
