@@ -134,11 +134,18 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode, lazy) if (cfg.graphs and hook is None) else None
     if graphs is not None and not graphs.usable():
         graphs = None
+    # the "noise" seed leaves Q(1) unnormalised (eigensolvers.f90:195-203); the reference's MGS2
+    # then projects against it as it stands, so its basis is not orthonormal (a projection onto an
+    # unnormalised vector removes only part of the component) and classical and modified
+    # Gram–Schmidt no longer agree.  That mode therefore runs the reference's own operation order.
+    mode = "mgs2" if (cfg.seed_mode == "noise" and start is None) else cfg.mode
+    if mode != cfg.mode:
+        graphs, lazy = None, False
     while True:
         if graphs is not None:
             graphs.run(mstart, k, transpose)
         else:
-            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=cfg.mode, transpose=transpose, on_step=hook,
+            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose, on_step=hook,
                                   lazy=lazy)
         H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
         ctx.check_nan()

@@ -334,3 +334,49 @@ def test_graph_replay_is_bit_identical(gpu, opname, mode):
     assert r1.schur_cnt == r2.schur_cnt and r1.schur_cnt >= 1
     np.testing.assert_array_equal(r1.vals, r2.vals)
     np.testing.assert_array_equal(r1.H, r2.H)
+
+
+def test_krylov_schur_knobs(gpu):
+    """Solver knobs beyond the defaults, config-1 operator (k_dim=16, schur_tgt=5):
+    seed_mode "noise" (Q(1) = A seed/||seed||, not renormalised, eigensolvers.f90:195-203) and
+    "as_is" against the oracle fed the same first vector; max_restarts caps the loop;
+    faithful_select=False keeps exactly the nev+4 largest (plus the |lambda| >= 1 - delta set)."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=32)
+    L = olayout(lay)
+    d, exact = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    dref = syn.to_reference_order(lay, d)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    s_ref = syn.to_reference_order(lay, syn.hash_vector(lay, 11))
+    # noise seed: q1 = A (s / ||s||_k_dot)
+    sn = s_ref.copy()
+    orc.k_normalize(L, w, sn)
+    q1 = np.zeros(L.len)
+    orc.lib().orc_op_diag(ctypes.byref(L.c), dref, sn, q1, 0.0)
+    res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise"))
+    ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
+    _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
+    # as_is: the caller's vector is the first basis vector
+    q1 = orc.prepare_seed(L, w, s_ref)
+    seed2 = ctx.vector().from_packed(syn.from_reference_order(lay, q1))
+    res = krylov_schur(ctx, op, seed2, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="as_is"))
+    ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
+    _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
+    # max_restarts
+    res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=6, max_restarts=1))
+    assert res.schur_cnt == 1 and len(res.mstart_history) == 1
+    # faithful_select=False: every restart keeps the nev+4 largest |lambda| (and the conjugate fix)
+    kept = []
+
+    def on_restart(cnt, mstart):
+        kept.append(mstart)
+
+    res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, faithful_select=False),
+                       on_restart=on_restart)
+    for sel in res.selected_history:
+        assert sel.sum() >= 5 + 4
+    assert res.converged >= 5
+    np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
