@@ -380,3 +380,37 @@ def test_krylov_schur_knobs(gpu):
         assert sel.sum() >= 5 + 4
     assert res.converged >= 5
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
+
+
+@pytest.mark.parametrize("findiff", [False, True])
+def test_gmres_restarts_vs_oracle(gpu, findiff):
+    """ts_gmres with a small Krylov space so the outer loop restarts (newton_krylov.f90:230-299):
+    k_dim=8, maxiter=12 — inner and outer residual histories against the oracle (1e-8 relative),
+    the same exits (findiff's relaxed 1e-8 inner / 1e-6 outer thresholds included), the solution
+    to 1e-10 in the W-norm."""
+    lay = cylinder_layout(200)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    op = ShiftedOperator(DiagOperator(ctx, d), -1.0)
+    rhs = ctx.vector()
+    rhs.fill_hash(3)
+    sol = ctx.vector()
+    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=8, maxiter=12, tol=1e-12, findiff=findiff))
+    J = syn.to_reference_order(lay, d) - 1.0
+
+    def mv(x, y):
+        y[:] = J * x
+        y[-1] = 0.0
+
+    rref = syn.to_reference_order(lay, syn.hash_vector(lay, 3))
+    sref, hist = orc.ts_gmres(L, w, mv, rref, maxiter=12, ksize=8, tol=1e-12, findiff=findiff)
+    assert len(info.outer_residuals) == len(hist["outer"]) >= 2
+    assert len(info.inner_residuals) == len(hist["inner"])
+    np.testing.assert_allclose(info.inner_residuals, hist["inner"], rtol=1e-8)
+    np.testing.assert_allclose(info.outer_residuals, hist["outer"], rtol=1e-8)
+    got = syn.to_reference_order(lay, sol.to_packed())
+    nw = L.nwf * L.nv
+    diff = got[:nw] - sref[:nw]
+    assert np.sqrt(np.sum(np.tile(w, L.nwf) * diff * diff)) < 1e-10
