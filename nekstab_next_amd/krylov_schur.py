@@ -157,6 +157,11 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
             break
         schur_cnt += 1
         mstart, selected = schur_condensation(ctx, H, Q, k, cfg)
+        if ctx.time_in_dot and mode != "mgs2":
+            # the restart moves the fields but not `time` (eigensolvers.f90:421-432, 458-459), so
+            # with time in k_dot (uparam(1)==2.1) the kept basis is no longer orthonormal: from here
+            # on the reference's MGS2 order is mirrored (CGS2/DCGS2 assume an orthonormal basis)
+            mode, graphs, lazy = "mgs2", None, False
         res.mstart_history.append(mstart)
         res.selected_history.append(selected)
         Hd.upload(H)

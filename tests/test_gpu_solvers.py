@@ -414,3 +414,27 @@ def test_gmres_restarts_vs_oracle(gpu, findiff):
     nw = L.nwf * L.nv
     diff = got[:nw] - sref[:nw]
     assert np.sqrt(np.sum(np.tile(w, L.nwf) * diff * diff)) < 1e-10
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+def test_krylov_schur_time_component_with_restarts(gpu, mode):
+    """uparam(1)==2.1 (the time slot inside k_dot) through Krylov–Schur restarts: the restart
+    rotation and Q(mstart) <- Q(k+1) move the fields only, not time (eigensolvers.f90:421-432,
+    458-459), as the oracle does; restart trajectory and Ritz values match it (1e-10).  The seed
+    goes in as given (seed_mode "as_is"), normalised in the k_dot norm that includes time."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=32, time_in_dot=True)
+    L = olayout(lay, time_in_dot=True)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d, time_scale=0.7)
+    q0 = syn.to_reference_order(lay, syn.hash_vector(lay, 5))
+    q0[-1] = 0.3
+    orc.k_normalize(L, w, q0)
+    seed = ctx.vector().from_packed(syn.from_reference_order(lay, q0))
+    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, mode=mode, seed_mode="as_is")
+    res = krylov_schur(ctx, op, seed, cfg)
+    dref = syn.to_reference_order(lay, d)
+    ref = orc.krylov_schur(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), q0, 16, 5)
+    assert res.schur_cnt >= 1
+    _compare_ks(res, ref, cfg)
