@@ -142,3 +142,64 @@ def test_rccl_collective_path_single_gpu(gpu, tmp_path):
                        timeout=300, env=env)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert "RCCL path ok" in p.stdout
+
+
+def _run_time(world_rank_pair, out, port):
+    """Arnoldi (DCGS2 and CGS2, m=20) with the time slot inside k_dot on a sharded layout: the
+    replicated scalar enters the dots on rank 0 only and follows every update on every rank."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.layout import NekLayout
+        from nekstab_next_amd.operators import DiagOperator
+        from nekstab_next_amd.vector import NekContext, k_normalize
+
+        lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=101).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=24, time_in_dot=True)
+        d, _ = syn.diag_spectrum(lay)
+        op = DiagOperator(ctx, d, time_scale=0.7)
+        res = {}
+        for mode in ("dcgs2", "cgs2"):
+            Q = ctx.basis(21)
+            Q[0].fill_hash(5)
+            Q[0].time = 0.3
+            k_normalize(Q[0])
+            Hd = HessenbergDev(ctx, 20)
+            arnoldi_factorization(ctx, op, Q, Hd, 1, 20, mode=mode)
+            res[mode] = (Hd.download(), Q.storage[:, lay.time_offset].cpu().numpy())
+        out[(world, rank)] = res
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_ranks_match_one_rank_with_time_in_dot(gpu):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_time, args=((0, 1), out, _free_port()))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    port = _free_port()
+    procs = [ctx.Process(target=_run_time, args=((r, 3), out, port)) for r in range(3)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    for mode in ("dcgs2", "cgs2"):
+        H1, t1 = out[(1, 0)][mode]
+        for rank in range(3):
+            H, t = out[(3, rank)][mode]
+            assert np.max(np.abs(H - H1)) <= 1e-12 * np.max(np.abs(H1)), (mode, rank)
+            np.testing.assert_allclose(t, t1, rtol=1e-11, atol=1e-15)   # replicated time, identical on every rank
+            assert np.any(np.abs(t) > 1e-3)
