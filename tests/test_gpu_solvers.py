@@ -438,3 +438,31 @@ def test_krylov_schur_time_component_with_restarts(gpu, mode):
     ref = orc.krylov_schur(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), q0, 16, 5)
     assert res.schur_cnt >= 1
     _compare_ks(res, ref, cfg)
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+def test_krylov_space_closing_early(gpu, mode):
+    """An operator with two distinct eigenvalues: the Krylov space closes after two steps in exact
+    arithmetic.  In floating point the projected f is rounding noise, not zero, and the reference
+    normalises it and carries on (a breakdown is only an exact zero norm, which aborts through the
+    NaN check, nek_vectors.f90:108-111); so does the product — no error, both eigenvalues converged
+    to 1e-12, in agreement with the oracle."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=20)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16)
+    d = np.zeros(lay.ld)
+    for f in range(lay.n_wf):
+        d[f * lay.sv: f * lay.sv + lay.n_v] = 0.5 if f == 0 else 0.25
+    d[lay.n_wf * lay.sv: lay.n_wf * lay.sv + lay.n_p] = 0.5
+    seed = ctx.vector()
+    seed.fill_hash(3)
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=8, schur_tgt=2, mode=mode))
+    conv = res.vals[res.residual < 1e-6]
+    for lam in (0.5, 0.25):
+        assert np.min(np.abs(conv - lam)) < 1e-12
+    L = olayout(lay)
+    q1 = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 3)))
+    ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 8, 2)
+    rconv = ref["vals"][ref["residual"] < 1e-6]
+    for lam in (0.5, 0.25):
+        assert np.min(np.abs(rconv - lam)) < 1e-12
