@@ -87,6 +87,29 @@ def set_threads(n: int) -> None:
     lib().orc_set_threads(int(n))
 
 
+_prod = None
+
+
+def prod_lib():
+    """The same restatement built with the reference's deployment flags (-Ofast -ffast-math,
+    bin/mks:53-55): the timed CPU baseline only (bench.py).  Reassociated sums, so never the
+    parity checker."""
+    global _prod
+    if _prod is None:
+        path = os.path.join(_HERE, "liboracle_prod.so")
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        L = ctypes.CDLL(path)
+        for k, (r, a) in _SIGS.items():
+            f = getattr(L, k)
+            f.restype = r
+            f.argtypes = a
+        _prod = L
+    return _prod
+
+
 _cgs2 = None
 
 
