@@ -98,6 +98,10 @@ namespace {
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
+#ifndef NKV_QTILE_EXP
+#define NKV_QTILE_EXP 0  // timing experiment only (wrong results): > 0 reads the basis of the multi-dot and
+                         // the dual update as tile-interleaved with this many columns per row tile
+#endif
 
 constexpr int kThreads = 256;                       // 4 waves of 64
 constexpr int kStreamUnr = NKV_STREAM_UNR;
@@ -621,7 +625,12 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
                 }
             }
             const int jl = x_last ? j - 1 : j;   // columns streamed from Q
+#if NKV_QTILE_EXP   // timing experiment (see dcgs2_tile)
+            const double* qb = Q + (fb + r0 - 2 * (int64_t)threadIdx.x) * NKV_QTILE_EXP + 2 * threadIdx.x;
+            ld = kTile;
+#else
             const double* qb = Q + fb + r0;
+#endif
             for (int c = 0; c < jl; c += U) {
                 double2 q[U][kPairs];
 #pragma unroll
@@ -900,7 +909,13 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         const double2 fv = ld2(win + r0 + k * 2 * kThreads);
         af[k] = make_double2(fv.x * wsc, fv.y * wsc);
     }
+#if NKV_QTILE_EXP   // timing experiment: tile-interleaved basis (the m columns of a row tile adjacent)
+    constexpr int kT = kThreads * kPairs * 2;
+    const double* qb = Q + (r0 - 2 * (int64_t)threadIdx.x) * NKV_QTILE_EXP + 2 * threadIdx.x;
+    ld = kT;
+#else
     const double* qb = Q + r0;
+#endif
     constexpr int U = NKV_DC_U;
     int c = 0;
     for (; c + U <= m; c += U) {

@@ -108,6 +108,7 @@ VARIANTS = {
     "d2u4": {"NKV_D2_U": 4},
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
     "d2red": {"NKV_D2_RED": 1},
+    "qtile": {"NKV_QTILE_EXP": 129},
 }
 
 
