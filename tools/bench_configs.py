@@ -49,6 +49,31 @@ def main():
         print(json.dumps(dict(config="config2", N=lay.N, k_dim=64, mode=mode, graphs=graphs, seconds=round(dt, 4),
                               arnoldi_steps=steps, ms_per_step=round(dt / steps * 1e3, 4),
                               restarts=r.schur_cnt, converged=int(conv.sum()), max_err_vs_exact=err)), flush=True)
+    # the rows above time a whole solve; with graphs=True that includes the one-off capture (the
+    # solve converges in its first factorisation, so the graph is never replayed).  Here the same
+    # 64-step DCGS2 factorisation is timed eager and as a graph replay (captured beforehand)
+    from nekstab_next_amd.arnoldi import FactorizationGraph, HessenbergDev, arnoldi_factorization
+    from nekstab_next_amd.krylov_schur import prepare_seed
+
+    Q2, Hd2, f2 = ctx.basis(65), HessenbergDev(ctx, 64), ctx.vector()
+    fg = FactorizationGraph(ctx, op, Q2, Hd2, f2, "dcgs2")
+    for how in ("eager", "graph", "eager", "graph"):
+        prepare_seed(seed, Q2[0])
+        if how == "graph" and (1, 64, False) not in fg.graphs:
+            fg.run(1, 64)   # capture (+ first replay), untimed
+            prepare_seed(seed, Q2[0])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            if how == "graph":
+                fg.run(1, 64)
+            else:
+                arnoldi_factorization(ctx, op, Q2, Hd2, 1, 64, f=f2, mode="dcgs2")
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 5
+        print(json.dumps(dict(config="config2_factorisation", N=lay.N, steps=64, mode="dcgs2", launch=how,
+                              ms=round(dt * 1e3, 3), ms_per_step=round(dt / 64 * 1e3, 4))), flush=True)
+    del Q2, Hd2, f2, fg
 
     # config 3's Krylov–Schur leg at BASELINE size (N=100,014,464, k_dim=128, schur_tgt=4): the
     # shift-invert spectrum and the config-1 diagonal spectrum scaled up converge in the first
