@@ -41,3 +41,17 @@ def test_cpu_cgs2_matches_mgs2_hessenberg():
         Hs.append(H)
     for H in Hs[1:]:
         np.testing.assert_allclose(H, Hs[0], rtol=0, atol=1e-12 * np.abs(Hs[0]).max())
+
+
+def test_bench_cpu_baseline_leg_small():
+    """bench.py's cpu_baseline leg on a tiny sample (CPU only): the reported object keeps the
+    contract's keys and names the build it timed."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    import bench
+
+    for variant in ("mgs2", "cgs2"):
+        r = bench.cpu_baseline(8, 6, 2, 5.0, variant=variant)
+        assert {"value", "unit", "cores", "kind", "sample"} <= set(r)
+        assert r["unit"] == "GB/s" and r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+        assert "steps j=1..6 of m=6" in r["sample"]
+    assert "-Ofast" in bench.cpu_baseline(8, 4, 1, 5.0)["sample"]
