@@ -98,6 +98,9 @@ namespace {
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
+#ifndef NKV_D2_FIELDMAJOR
+#define NKV_D2_FIELDMAJOR 0  // 1: the two-vector multi-dot sweeps the weighted fields one after another
+#endif
 #ifndef NKV_QTILE_EXP
 #define NKV_QTILE_EXP 0  // timing experiment only (wrong results): > 0 reads the basis of the multi-dot and
                          // the dual update as tile-interleaved with this many columns per row tile
@@ -594,12 +597,21 @@ __global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restric
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
+#if NKV_D2_FIELDMAJOR
+    // field-major order: the whole grid sweeps one field before the next, so the pages in use at
+    // once are those of one field of each column (the weights are re-read once per field)
+    for (int fo = 0; fo < n_fields; ++fo)
+#endif
     for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_per_field; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
         for (int k = 0; k < kPairs; ++k) wv[k] = ld2(w + r0 + k * 2 * kThreads);
+#if NKV_D2_FIELDMAJOR
+        for (int fi = fo; fi < fo + 1; ++fi) {
+#else
         for (int fi = 0; fi < n_fields; ++fi) {
+#endif
             const int64_t fb = (int64_t)(blockIdx.y * n_fields + fi) * sv;
             double2 wx[kPairs], wy[kPairs];
             double sxx = 0.0, sxy = 0.0;

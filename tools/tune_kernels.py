@@ -109,6 +109,9 @@ VARIANTS = {
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
     "d2red": {"NKV_D2_RED": 1},
     "qtile": {"NKV_QTILE_EXP": 129},
+    "d2_fmaj": {"NKV_D2_FIELDMAJOR": 1},
+    "d2_fmaj_b512": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 512},
+    "d2_fmaj_b1024": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 1024},
 }
 
 
