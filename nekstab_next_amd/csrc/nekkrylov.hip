@@ -98,6 +98,9 @@ namespace {
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
+#ifndef NKV_LD_ALIGN
+#define NKV_LD_ALIGN NKV_TILE  // required multiple of the basis stride (2 in the stride experiment)
+#endif
 #ifndef NKV_D2_FIELDMAJOR
 #define NKV_D2_FIELDMAJOR 0  // 1: the two-vector multi-dot sweeps the weighted fields one after another
 #endif
@@ -176,7 +179,7 @@ int check_layout(const nkv_layout* L) {
     if (L->n_wf < 1 || L->n_v < 0 || L->n_p < 0)
         return fail(NKV_EINVAL, "bad layout: n_wf=%d n_v=%lld n_p=%lld", L->n_wf,
                     (long long)L->n_v, (long long)L->n_p);
-    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % NKV_TILE || L->sp % NKV_TILE || L->ld % NKV_TILE)
+    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % NKV_TILE || L->sp % NKV_TILE || L->ld % NKV_LD_ALIGN)
         return fail(NKV_ESHAPE, "layout not padded to NKV_TILE: sv=%lld sp=%lld ld=%lld",
                     (long long)L->sv, (long long)L->sp, (long long)L->ld);
     if (L->ld < rows_of(L) + 1)

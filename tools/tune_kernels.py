@@ -110,6 +110,7 @@ VARIANTS = {
     "d2red": {"NKV_D2_RED": 1},
     "qtile": {"NKV_QTILE_EXP": 129},
     "d2_fmaj": {"NKV_D2_FIELDMAJOR": 1},
+    "ldany": {"NKV_LD_ALIGN": 2},
     "d2_fmaj_b512": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 512},
     "d2_fmaj_b1024": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 1024},
 }
@@ -150,7 +151,8 @@ def run(names, E, rounds, js, only=None):
     jmax = max(js)
     dev = torch.device("cuda", 0)
     Lc = lay.c_struct()
-    ldpad = int(os.environ.get("NKV_TUNE_LDPAD", "0"))   # extra doubles of column stride (multiple of 4096)
+    ldpad = int(os.environ.get("NKV_TUNE_LDPAD", "0"))   # extra doubles of column stride (multiple of 4096,
+    # or any even number with the "ldany" build)
     Lc.ld += ldpad
     Lp = ctypes.byref(Lc)
     Q = torch.empty((jmax + 1, Lc.ld), dtype=torch.float64, device=dev)
