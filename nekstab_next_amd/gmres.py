@@ -25,7 +25,6 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 import numpy as np
-import torch
 
 from . import lapack
 from .arnoldi import HessenbergDev, arnoldi_factorization

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import NKV_NORM2, NKV_OVERWRITE, NKV_TIME
+from ._lib import NKV_OVERWRITE, NKV_TIME
 from .comm import Comm
 from .layout import NekLayout
 

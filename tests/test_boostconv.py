@@ -51,8 +51,6 @@ def test_boostconv_oracle_converges_to_fixed_point():
 
 @pytest.mark.gpu
 def test_boostconv_device_matches_oracle(gpu):
-    import torch
-
     from nekstab_next_amd.boostconv import BoostConv, velocity_layout
     from nekstab_next_amd.vector import NekContext
 

@@ -13,7 +13,7 @@ import torch
 import oracle as orc
 from helpers import olayout
 from nekstab_next_amd import synthetic as syn
-from nekstab_next_amd._lib import NKV_NORM2, NKV_OVERWRITE, NKV_TIME, NkvError, NkvNaNError
+from nekstab_next_amd._lib import NKV_NORM2, NKV_TIME, NkvError, NkvNaNError
 from nekstab_next_amd.arnoldi import HessenbergDev, arnoldi_factorization
 from nekstab_next_amd.layout import NekLayout
 from nekstab_next_amd.operators import DiagOperator, Rot2Operator

@@ -4,7 +4,6 @@ algorithms to exact answers: dense W-weighted SVD / eigen-decomposition of small
 exact solution of a diagonal system."""
 import numpy as np
 import pytest
-import torch
 
 from nekstab_next_amd import synthetic as syn
 from nekstab_next_amd.krylov_schur import prepare_seed

@@ -6,10 +6,8 @@ solutions are exact, and against the one recorded run of the real reference (SUR
 "Verified runs" (2): k_dim=16, schur_tgt=5, diag(0.99..0.89, bulk): 2 Schur condensations with
 9 eigenvalues selected each, 6 converged, residuals 3e-11..3e-9).
 """
-import ctypes
 
 import numpy as np
-import pytest
 
 import oracle as orc
 from helpers import olayout, oracle_diag_matvec, oracle_rot2_matvec
