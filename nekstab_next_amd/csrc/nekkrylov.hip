@@ -98,6 +98,9 @@ namespace {
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
+#ifndef NKV_DC_SCHED
+#define NKV_DC_SCHED 0  // dual update load schedule: 1 sched_barrier after each step's loads, 2 waves_per_eu <= 3
+#endif
 #ifndef NKV_LD_ALIGN
 #define NKV_LD_ALIGN NKV_TILE  // required multiple of the basis stride (2 in the stride experiment)
 #endif
@@ -939,6 +942,11 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
+#if NKV_DC_SCHED == 1
+        // keep all U*kPairs loads of this step in flight before the first FMA waits on one (the
+        // default schedule interleaves them with the FMAs to stay at 128 VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double ac = -a[c + u], xc = -x[c + u];
@@ -983,7 +991,11 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
 // kNrm = false: no ||f||_W^2 partial (the next step's dot of u with itself supplies beta^2, see
 // nkv_dcgs2_coef), so the weights are not read and no partials are written.
 template <int kPairs, bool kNrm>
-__global__ __launch_bounds__(kThreads) void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
+__global__ __launch_bounds__(kThreads)
+#if NKV_DC_SCHED == 2
+__attribute__((amdgpu_waves_per_eu(1, 3)))
+#endif
+void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
                                                            const double* __restrict__ coef,
                                                            double* __restrict__ qj, const double* __restrict__ win,
                                                            double* __restrict__ f,

@@ -110,6 +110,11 @@ VARIANTS = {
     "qtile": {"NKV_QTILE_EXP": 129},
     "d2_fmaj": {"NKV_D2_FIELDMAJOR": 1},
     "ldany": {"NKV_LD_ALIGN": 2},
+    "dc_sched1": {"NKV_DC_SCHED": 1},
+    "dc_sched2": {"NKV_DC_SCHED": 2},
+    "dc_sched1_u4": {"NKV_DC_SCHED": 1, "NKV_DC_U": 4},
+    "dc_sched2_g512": {"NKV_DC_SCHED": 2, "NKV_DC_G": 512},
+    "dc_sched2_g1024": {"NKV_DC_SCHED": 2, "NKV_DC_G": 1024},
     "d2_fmaj_b512": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 512},
     "d2_fmaj_b1024": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 1024},
 }
