@@ -98,6 +98,9 @@ namespace {
 #ifndef NKV_XCD_MAP
 #define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
 #endif
+#ifndef NKV_D2_SCHED
+#define NKV_D2_SCHED 0  // > 0: two-vector multi-dot compiled for this many waves per SIMD (register budget)
+#endif
 #ifndef NKV_DC_SCHED
 #define NKV_DC_SCHED 0  // dual update load schedule: 1 sched_barrier after each step's loads, 2 waves_per_eu <= 3
 #endif
@@ -587,7 +590,11 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 // read of Q (x = the provisional q_j, y = A q_j).  Same grid and tiling as k_block_dot.
 // ------------------------------------------------------------------------------------------
 template <int kPairs>
-__global__ __launch_bounds__(kThreads) void k_block_dot2(const double* __restrict__ Q, int64_t ld,
+__global__ __launch_bounds__(kThreads)
+#if NKV_D2_SCHED
+__attribute__((amdgpu_waves_per_eu(NKV_D2_SCHED, NKV_D2_SCHED)))
+#endif
+void k_block_dot2(const double* __restrict__ Q, int64_t ld,
                                                          int j, const double* __restrict__ x,
                                                          const double* __restrict__ y,
                                                          const double* __restrict__ w, int64_t sv,

@@ -114,6 +114,10 @@ VARIANTS = {
     "dc_sched2": {"NKV_DC_SCHED": 2},
     "dc_sched1_u4": {"NKV_DC_SCHED": 1, "NKV_DC_U": 4},
     "dc_sched2_g512": {"NKV_DC_SCHED": 2, "NKV_DC_G": 512},
+    "d2_sched4": {"NKV_D2_SCHED": 4},
+    "d2_sched4_b512": {"NKV_D2_SCHED": 4, "NKV_D2_MAXB": 512},
+    "d2_sched4_b1024": {"NKV_D2_SCHED": 4, "NKV_D2_MAXB": 1024},
+    "d2_sched3_b768": {"NKV_D2_SCHED": 3, "NKV_D2_MAXB": 768},
     "dc_sched2_g1024": {"NKV_DC_SCHED": 2, "NKV_DC_G": 1024},
     "d2_fmaj_b512": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 512},
     "d2_fmaj_b1024": {"NKV_D2_FIELDMAJOR": 1, "NKV_D2_MAXB": 1024},
