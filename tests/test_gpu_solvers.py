@@ -466,3 +466,28 @@ def test_krylov_space_closing_early(gpu, mode):
     rconv = ref["vals"][ref["residual"] < 1e-6]
     for lam in (0.5, 0.25):
         assert np.min(np.abs(rconv - lam)) < 1e-12
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+def test_factorisation_is_run_to_run_deterministic(gpu, mode):
+    """Every reduction is a fixed-order two-stage sum (no atomics), so the same factorisation on
+    the same inputs gives the same bits: H and the whole basis, at a size with thousands of
+    workgroup tiles (E=8000, N=1.8e7, m=48)."""
+    from nekstab_next_amd.krylov_schur import prepare_seed
+
+    lay = box3d_layout(8000)
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), max_cols=49)
+    d, _ = syn.laplacian_shift_invert(lay)
+    op = DiagOperator(ctx, d)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    runs = []
+    for _ in range(2):
+        Q, Hd, f = ctx.basis(49), HessenbergDev(ctx, 48), ctx.vector()
+        prepare_seed(seed, Q[0])
+        arnoldi_factorization(ctx, op, Q, Hd, 1, 48, f=f, mode=mode)
+        runs.append((Hd.download(), Q))
+    (H1, Q1), (H2, Q2) = runs
+    np.testing.assert_array_equal(H1, H2)
+    assert np.all(np.abs(np.diag(H1, -1)) > 0)
+    assert torch.equal(Q1.storage, Q2.storage)
