@@ -472,7 +472,7 @@ def test_krylov_space_closing_early(gpu, mode):
 def test_factorisation_is_run_to_run_deterministic(gpu, mode):
     """Every reduction is a fixed-order two-stage sum (no atomics), so the same factorisation on
     the same inputs gives the same bits: H and the whole basis, at a size with thousands of
-    workgroup tiles (E=8000, N=1.8e7, m=48)."""
+    workgroup tiles (E=8000, N=18,112,000, m=48)."""
     from nekstab_next_amd.krylov_schur import prepare_seed
 
     lay = box3d_layout(8000)
