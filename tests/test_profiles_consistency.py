@@ -1,0 +1,50 @@
+"""The committed measurement artefacts agree with each other (CPU only, no GPU): the latest
+bench line's dominant-kernel timing (HIP events inside bench.py) matches the rocprofv3 --stats
+summary of the same command, and its `roofline.traffic` agrees with the PMC figure in
+profiles/traffic_latest.json, which is within 1 % of the algorithmic bytes (no wasted re-reads)."""
+import csv
+import json
+import os
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+PROF = os.path.join(ROOT, "profiles")
+LATEST = "r01u"
+KEY = {"dcgs2_update": "k_dcgs2_update<", "block_dot2": "k_block_dot2<"}
+
+
+def _load():
+    bench = json.load(open(os.path.join(PROF, f"{LATEST}_bench_n1.json")))
+    stats = list(csv.DictReader(open(os.path.join(PROF, f"{LATEST}_bench_n1_kernel_stats.csv"))))
+    return bench, stats
+
+
+def test_bench_line_contract_fields():
+    bench, _ = _load()
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in bench, k
+    r = bench["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert bench["cpu_baseline"]["kind"] == "port" and bench["cpu_baseline"]["cores"] >= 1
+
+
+def test_events_agree_with_rocprof():
+    bench, stats = _load()
+    for fam, key in KEY.items():
+        rows = [r for r in stats if key in r["Name"]]
+        avg_ms = sum(float(r["TotalDurationNs"]) for r in rows) / sum(int(r["Calls"]) for r in rows) / 1e6
+        ev = bench["phases"][fam]["avg_ms"]
+        assert abs(ev / avg_ms - 1.0) < 0.02, (fam, ev, avg_ms)
+
+
+def test_pmc_traffic_matches_algorithmic_bytes():
+    bench, _ = _load()
+    t = json.load(open(os.path.join(PROF, "traffic_latest.json")))
+    r = bench["roofline"]
+    assert t["kernel_family"] == r["kernel"]
+    # the bench reads traffic_latest.json as it stood when it ran (the previous PMC pass of the same
+    # kernel); the pass collected alongside it must agree
+    assert abs(r["traffic"] / t["hbm_bytes_per_launch"] - 1.0) < 1e-4
+    assert abs(t["hbm_bytes_per_launch"] / t["algorithmic_bytes_per_launch"] - 1.0) < 0.01
+    assert abs(t["algorithmic_bytes_per_launch"] / r["avg_bytes_per_launch"] - 1.0) < 1e-9
