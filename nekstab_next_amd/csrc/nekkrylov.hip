@@ -58,16 +58,10 @@ namespace {
 #ifndef NKV_STREAM_UNR
 #define NKV_STREAM_UNR 4  // double2 per thread in flight in the streaming vector kernels
 #endif
-#ifndef NKV_DC_EXPERIMENT
-#define NKV_DC_EXPERIMENT 0
-#endif
 #ifndef NKV_DC_G
 #define NKV_DC_G 768  // workgroups of the DCGS2 dual update: 3 per CU (122 VGPRs allow 4) is 1-6 %
                       // faster than 4 per CU at N=1e8 and at the 8-GPU shard; non-multiples of the
                       // 256 CUs lose 5-10 % (profiles/r01k_tune_update_grid.log)
-#endif
-#ifndef NKV_DC_FIELDLOOP
-#define NKV_DC_FIELDLOOP 1  // DCGS2 dual update: one block walks all weighted fields of a row tile
 #endif
 #ifndef NKV_D2_MAXB
 #define NKV_D2_MAXB 256  // workgroups of the two-vector multi-dot: one per CU (+1 % over 1024 at
@@ -79,40 +73,13 @@ namespace {
 #ifndef NKV_D2_U
 #define NKV_D2_U 2  // basis columns in flight in the two-vector multi-dot
 #endif
-#ifndef NKV_FUSE_PF
-#define NKV_FUSE_PF 0  // 1: prefetch the next tile's columns across the per-tile barrier
-#endif
-#ifndef NKV_DC_SYNC
-#define NKV_DC_SYNC 0  // experiment: align the dual update's store phases over the grid (soft barrier)
-#endif
-#ifndef NKV_DC_SYNC_PCT
-#define NKV_DC_SYNC_PCT 100  // ... a block waits for this percentage of the grid (quorum)
-#endif
-#ifndef NKV_DC_SYNC_US
-#define NKV_DC_SYNC_US 20  // ... longest wait per round (us) before a block stores anyway
-#endif
-#ifndef NKV_ST_AUX
-#define NKV_ST_AUX -1  // stores of the dual update / op_diag: -1 nontemporal global store; >= 0 buffer
-                       // store with this cache policy (1 sc0, 2 nt, 16 sc1, 17 sc0 sc1, 18 nt sc1)
-#endif
-#ifndef NKV_XCD_MAP
-#define NKV_XCD_MAP 0  // 1: XCD-contiguous tile order in the multi-dot, the dual update and op_diag
-#endif
-#ifndef NKV_D2_SCHED
-#define NKV_D2_SCHED 0  // > 0: two-vector multi-dot compiled for this many waves per SIMD (register budget)
-#endif
-#ifndef NKV_DC_SCHED
-#define NKV_DC_SCHED 0  // dual update load schedule: 1 sched_barrier after each step's loads, 2 waves_per_eu <= 3
-#endif
-#ifndef NKV_LD_ALIGN
-#define NKV_LD_ALIGN NKV_TILE  // required multiple of the basis stride (2 in the stride experiment)
-#endif
-#ifndef NKV_D2_FIELDMAJOR
-#define NKV_D2_FIELDMAJOR 0  // 1: the two-vector multi-dot sweeps the weighted fields one after another
-#endif
-#ifndef NKV_QTILE_EXP
-#define NKV_QTILE_EXP 0  // timing experiment only (wrong results): > 0 reads the basis of the multi-dot and
-                         // the dual update as tile-interleaved with this many columns per row tile
+// The round-1 timing experiments (store skipping, grid-wide soft barriers, tile-interleaved and
+// field-major sweeps, XCD tile maps, buffer-store cache policies, register-budget schedules;
+// DESIGN.md §6 "What did not help") are not part of this file.  The knobs above change speed only.
+#if defined(NKV_DC_EXPERIMENT) || defined(NKV_DC_SYNC) || defined(NKV_QTILE_EXP) || defined(NKV_D2_FIELDMAJOR) || \
+    defined(NKV_DC_SCHED) || defined(NKV_D2_SCHED) || defined(NKV_ST_AUX) || defined(NKV_XCD_MAP) ||           \
+    defined(NKV_DC_FIELDLOOP) || defined(NKV_FUSE_PF) || defined(NKV_LD_ALIGN)
+#error "round-1 experiment switches were removed from the product kernel"
 #endif
 
 constexpr int kThreads = 256;                       // 4 waves of 64
@@ -124,16 +91,6 @@ constexpr int kMaxBlocks = NKV_MAXB;                 // reduction partial slots 
 constexpr int kColUnroll = NKV_COLU;                 // columns in flight per thread (block dot)
 constexpr size_t kCtrlBytes = 256;                   // control words at the head of the workspace
 constexpr int kRotMaxK = NKV_ROT_MAX_K;               // rotation: 64-row tiles up to k=256, 32-row beyond
-
-// Tile order of a grid-stride loop.  Blocks b and b+8 share an XCD (round-robin dispatch,
-// MI355X_MICROARCH.md §Workgroup dispatch); with NKV_XCD_MAP the G/8 blocks of one XCD take
-// consecutive tiles of every round.  A permutation of [0, G): speed only, any placement is correct.
-__device__ __forceinline__ int tile_block(int b, int G) {
-#if NKV_XCD_MAP
-    if ((G & 7) == 0) return (b & 7) * (G >> 3) + (b >> 3);
-#endif
-    return b;
-}
 
 thread_local char g_err[512] = "";
 
@@ -185,7 +142,7 @@ int check_layout(const nkv_layout* L) {
     if (L->n_wf < 1 || L->n_v < 0 || L->n_p < 0)
         return fail(NKV_EINVAL, "bad layout: n_wf=%d n_v=%lld n_p=%lld", L->n_wf,
                     (long long)L->n_v, (long long)L->n_p);
-    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % NKV_TILE || L->sp % NKV_TILE || L->ld % NKV_LD_ALIGN)
+    if (L->sv < L->n_v || L->sp < L->n_p || L->sv % NKV_TILE || L->sp % NKV_TILE || L->ld % NKV_TILE)
         return fail(NKV_ESHAPE, "layout not padded to NKV_TILE: sv=%lld sp=%lld ld=%lld",
                     (long long)L->sv, (long long)L->sp, (long long)L->ld);
     if (L->ld < rows_of(L) + 1)
@@ -276,18 +233,6 @@ __device__ __forceinline__ double2 ldq(const double* p) {
 #endif
 }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
-// Store of one double2 at element offset `off` (< 2^29) of a streamed vector `base` (wave-uniform),
-// with the cache policy NKV_ST_AUX (a buffer store; -1: st2s below).
-typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st2s(double* p, double2 v);
-__device__ __forceinline__ void st2p(double* base, int64_t off, double2 v) {
-#if NKV_ST_AUX >= 0
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xFFFFFFFFu, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, v), r, (int)(off * 8), 0, NKV_ST_AUX);
-#else
-    st2s(base + off, v);
-#endif
-}
 // Stores of whole streamed vectors (800 MB at N=1e8, never re-read from cache): non-temporal (NKV_NT_ST)
 __device__ __forceinline__ void st2s(double* p, double2 v) {
 #if NKV_NT_ST
@@ -296,6 +241,8 @@ __device__ __forceinline__ void st2s(double* p, double2 v) {
     st2(p, v);
 #endif
 }
+// Store of one double2 at element offset `off` of a streamed vector `base`.
+__device__ __forceinline__ void st2p(double* base, int64_t off, double2 v) { st2s(base + off, v); }
 
 // ------------------------------------------------------------------------------------------
 // block weighted multi-dot:  partials[c][b] = sum over this block's tiles of q_c . (w f)
@@ -525,15 +472,9 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
         q[CPW - 1] = (wv + NW * (CPW - 1) < j) ? ldq(at_b(qcol[CPW - 1], rb)) : make_double2(0.0, 0.0);
     };
     double2 q[CPW];
-#if NKV_FUSE_PF
-    double2 qn[CPW];
-    if ((int64_t)blockIdx.x < tiles_total) load_tile(q, blockIdx.x);
-#endif
     for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x, buf ^= 1) {
         const uint32_t r = (uint32_t)(t * kFuseRows) + 2u * lane;
-#if !NKV_FUSE_PF
         load_tile(q, t);
-#endif
         double2 s = make_double2(0.0, 0.0);
 #pragma unroll
         for (int i = 0; i < CPW; ++i) {
@@ -546,14 +487,7 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
         // the prefetch would wait for it
         const double2 ww = weighted ? ld2(at_b(w, (r - (uint32_t)((t / tiles_per_field) * sv)) * 8u)) : make_double2(0.0, 0.0);
         part[buf][wv][lane] = s;
-#if NKV_FUSE_PF
-        const int64_t tn = t + gridDim.x;
-        if (tn < tiles_total) load_tile(qn, tn);  // stays in flight across the barrier below
-        // LDS-only wait + raw barrier: a __syncthreads() would also drain vmcnt (the prefetch)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
         __syncthreads();
-#endif
         double2 tot = part[buf][0][lane];
 #pragma unroll
         for (int k = 1; k < NW; ++k) {
@@ -568,10 +502,6 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 #pragma unroll
             for (int i = 0; i < CPW; ++i) acc[i] = fma(q[i].y, b, fma(q[i].x, a, acc[i]));
         }
-#if NKV_FUSE_PF
-#pragma unroll
-        for (int i = 0; i < CPW; ++i) q[i] = qn[i];
-#endif
         // no second barrier: the next tile writes the other buffer, and a wave can only reach the
         // barrier after it once every wave has passed this tile's barrier (and read this buffer)
     }
@@ -591,9 +521,6 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
 // ------------------------------------------------------------------------------------------
 template <int kPairs>
 __global__ __launch_bounds__(kThreads)
-#if NKV_D2_SCHED
-__attribute__((amdgpu_waves_per_eu(NKV_D2_SCHED, NKV_D2_SCHED)))
-#endif
 void k_block_dot2(const double* __restrict__ Q, int64_t ld,
                                                          int j, const double* __restrict__ x,
                                                          const double* __restrict__ y,
@@ -610,21 +537,12 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-#if NKV_D2_FIELDMAJOR
-    // field-major order: the whole grid sweeps one field before the next, so the pages in use at
-    // once are those of one field of each column (the weights are re-read once per field)
-    for (int fo = 0; fo < n_fields; ++fo)
-#endif
-    for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_per_field; t += gridDim.x) {
+    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
         for (int k = 0; k < kPairs; ++k) wv[k] = ld2(w + r0 + k * 2 * kThreads);
-#if NKV_D2_FIELDMAJOR
-        for (int fi = fo; fi < fo + 1; ++fi) {
-#else
         for (int fi = 0; fi < n_fields; ++fi) {
-#endif
             const int64_t fb = (int64_t)(blockIdx.y * n_fields + fi) * sv;
             double2 wx[kPairs], wy[kPairs];
             double sxx = 0.0, sxy = 0.0;
@@ -650,12 +568,7 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
                 }
             }
             const int jl = x_last ? j - 1 : j;   // columns streamed from Q
-#if NKV_QTILE_EXP   // timing experiment (see dcgs2_tile)
-            const double* qb = Q + (fb + r0 - 2 * (int64_t)threadIdx.x) * NKV_QTILE_EXP + 2 * threadIdx.x;
-            ld = kTile;
-#else
             const double* qb = Q + fb + r0;
-#endif
             for (int c = 0; c < jl; c += U) {
                 double2 q[U][kPairs];
 #pragma unroll
@@ -901,20 +814,6 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
     }
 }
 
-// Timing alignment only (NKV_DC_SYNC experiment): a block counts itself in and waits until
-// `target` blocks have arrived or NKV_DC_SYNC_US microseconds have passed, whichever is first, so
-// the wait always ends (no co-residency assumption) and no data crosses it.
-__device__ __forceinline__ void soft_barrier(int* ctr, int target) {
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-               __builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)NKV_DC_SYNC_US * 100)
-            __builtin_amdgcn_s_sleep(8);
-    }
-    __syncthreads();
-}
-
 // DCGS2 update, one read of Q_m (m columns):  qbar = (u s - Q_m a) * rinv  -> column m (in place),
 // f = (A u) s rinv - Q_m x - qbar * yc  -> fout (the next column: normalised one step later),
 // ||f||_W^2 partial.  One row tile (kTile rows at r0): returns f in af.
@@ -923,8 +822,7 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
                                            const double* __restrict__ a, const double* __restrict__ x,
                                            double rinv, double yc, double sc, double* __restrict__ qj,
                                            const double* __restrict__ win, double* __restrict__ f,
-                                           int64_t r0, double2 (&af)[kPairs], int* sync = nullptr,
-                                           int sync_target = 0) {
+                                           int64_t r0, double2 (&af)[kPairs]) {
     double2 aq[kPairs];
     const double wsc = sc * rinv;
 #pragma unroll
@@ -934,13 +832,7 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         const double2 fv = ld2(win + r0 + k * 2 * kThreads);
         af[k] = make_double2(fv.x * wsc, fv.y * wsc);
     }
-#if NKV_QTILE_EXP   // timing experiment: tile-interleaved basis (the m columns of a row tile adjacent)
-    constexpr int kT = kThreads * kPairs * 2;
-    const double* qb = Q + (r0 - 2 * (int64_t)threadIdx.x) * NKV_QTILE_EXP + 2 * threadIdx.x;
-    ld = kT;
-#else
     const double* qb = Q + r0;
-#endif
     constexpr int U = NKV_DC_U;
     int c = 0;
     for (; c + U <= m; c += U) {
@@ -949,11 +841,6 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int k = 0; k < kPairs; ++k) q[u][k] = ldq(qb + (int64_t)(c + u) * ld + k * 2 * kThreads);
-#if NKV_DC_SCHED == 1
-        // keep all U*kPairs loads of this step in flight before the first FMA waits on one (the
-        // default schedule interleaves them with the FMAs to stay at 128 VGPRs)
-        __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double ac = -a[c + u], xc = -x[c + u];
@@ -977,20 +864,12 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
             af[k].y = fma(xc, q.y, af[k].y);
         }
     }
-    if (sync) soft_barrier(sync, sync_target);
 #pragma unroll
     for (int k = 0; k < kPairs; ++k) {
         const double2 qbv = make_double2(aq[k].x * rinv, aq[k].y * rinv);
         af[k].x = fma(-yc, qbv.x, af[k].x);
         af[k].y = fma(-yc, qbv.y, af[k].y);
-        // NKV_DC_EXPERIMENT (timing only, wrong results): 1 skips both stores, 2 skips the q_j store
-#if NKV_DC_EXPERIMENT >= 1
-        if (af[k].x == 12345.678)
-#endif
         st2p(qj, r0 + k * 2 * kThreads, qbv);
-#if NKV_DC_EXPERIMENT == 1
-        if (af[k].x == 12345.678)
-#endif
         st2p(f, r0 + k * 2 * kThreads, af[k]);
     }
 }
@@ -999,9 +878,6 @@ __device__ __forceinline__ void dcgs2_tile(const double* __restrict__ Q, int64_t
 // nkv_dcgs2_coef), so the weights are not read and no partials are written.
 template <int kPairs, bool kNrm>
 __global__ __launch_bounds__(kThreads)
-#if NKV_DC_SCHED == 2
-__attribute__((amdgpu_waves_per_eu(1, 3)))
-#endif
 void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
                                                            const double* __restrict__ coef,
                                                            double* __restrict__ qj, const double* __restrict__ win,
@@ -1032,31 +908,16 @@ void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
     }
     double2 af[kPairs];
     if constexpr (!kNrm) {
-#if NKV_DC_SYNC
-        int* sync = reinterpret_cast<int*>(partials) - 16;   // the workspace's sync word (zeroed per launch)
-        const int rounds = (tiles_total + gridDim.x - 1) / gridDim.x;
-        const int quorum = (int)(((int64_t)gridDim.x * NKV_DC_SYNC_PCT) / 100);
-        for (int r = 0; r < rounds; ++r) {
-            const int t = tile_block(blockIdx.x, gridDim.x) + r * gridDim.x;
-            if (t < tiles_total)
-                dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af,
-                                   sync, r * gridDim.x + quorum);
-            else
-                soft_barrier(sync, r * gridDim.x + quorum);
-        }
-#else
-        for (int t = tile_block(blockIdx.x, gridDim.x); t < tiles_total; t += gridDim.x)
+        for (int t = blockIdx.x; t < tiles_total; t += gridDim.x)
             dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af);
-#endif
         return;
     }
     double nrm = 0.0;
-#if NKV_DC_FIELDLOOP
     // work unit = one row tile of EVERY weighted field (the norm's weights are read once per unit,
     // not once per field), then the pressure tiles one by one
     const int n_wf = tiles_per_field > 0 ? tiles_w / tiles_per_field : 0;
     const int n_units = tiles_per_field + (tiles_total - tiles_w);
-    for (int u = tile_block(blockIdx.x, gridDim.x); u < n_units; u += gridDim.x) {
+    for (int u = blockIdx.x; u < n_units; u += gridDim.x) {
         if (u < tiles_per_field) {
             double2 wv[kPairs];
 #pragma unroll
@@ -1075,21 +936,6 @@ void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
                                (int64_t)(tiles_w + u - tiles_per_field) * kTile + 2 * threadIdx.x, af);
         }
     }
-#else
-    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
-        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
-        dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, r0, af);
-        if (t < tiles_w) {
-            const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
-#pragma unroll
-            for (int k = 0; k < kPairs; ++k) {
-                const double2 wv = ld2(w + wr + k * 2 * kThreads);
-                nrm = fma(wv.x * af[k].x, af[k].x, nrm);
-                nrm = fma(wv.y * af[k].y, af[k].y, nrm);
-            }
-        }
-    }
-#endif
     nrm = block_sum(nrm, lds4);
     if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
 }
@@ -1533,7 +1379,7 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
                                                       double* __restrict__ y, int64_t rows,
                                                       int64_t time_off, double ts) {
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
-    for (int64_t ci = tile_block(blockIdx.x, gridDim.x); ci < chunks; ci += gridDim.x) {
+    for (int64_t ci = blockIdx.x; ci < chunks; ci += gridDim.x) {
         const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
         double2 dv[kStreamUnr], xv[kStreamUnr];
 #pragma unroll
@@ -2055,9 +1901,6 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
-#if NKV_DC_SYNC
-    if (!nrm2_dev) NKV_HIP(hipMemsetAsync(reinterpret_cast<int*>(part) - 16, 0, sizeof(int), st));
-#endif
     auto kern = large ? (nrm2_dev ? k_dcgs2_update<NKV_DC_PAIRS, true> : k_dcgs2_update<NKV_DC_PAIRS, false>)
                       : (nrm2_dev ? k_dcgs2_update<NKV_PAIRS_SMALL, true> : k_dcgs2_update<NKV_PAIRS_SMALL, false>);
     hipLaunchKernelGGL(kern, dim3(g), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj, win, fout, w, L->sv, tpf,
