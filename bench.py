@@ -5,31 +5,39 @@ BASELINE.json config 3: "Synthetic shift-invert Laplacian, N=1e8 dofs, m=128, ba
 MI355X GPUs with RCCL all-reduce" — 3-D spectral-element layout lx1=8, lx2=6, fields
 {vx, vy, vz, t} weighted + pressure, E=44,176 elements -> N = 100,014,464 doubles per vector
 (SURVEY.md §8(d)).  Total N is fixed for every GPU count (strong scaling): each rank owns an
-element-contiguous shard; dots are all-reduced (RCCL) once per Gram–Schmidt pass.
+element-contiguous shard; dots are all-reduced (RCCL) once per Arnoldi step.
+
+Launch.  ``python bench.py --gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment spawns N
+child processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT,
+as ``torch.distributed.run`` sets them) before anything touches the GPU, waits for them and exits
+with the worst child exit status (no exec).  Under ``torch.distributed.run`` the environment is
+already set and ``--gpus`` must equal ``WORLD_SIZE`` (else exit 2).  ``--dry-launch`` stops every
+rank before GPU initialisation and prints its rank environment (CPU test of the launcher).
 
 One *step* = one full m-step Arnoldi factorisation from the normalised seed (prepare_seed, then
-m x [synthetic matvec + block Gram–Schmidt + normalise], the closing re-orthogonalisation)
-followed by the host Ritz extraction (H download, dgeev, residuals) — the work of one
-Krylov–Schur cycle before any restart.
+m x [synthetic matvec + block Gram–Schmidt], the closing re-orthogonalisation) followed by the
+host Ritz extraction (H download, dgeev, residuals) — the work of one Krylov–Schur cycle before
+any restart.
 
 ``value`` = achieved HBM GB/s of the whole step: the bytes the executed algorithm moves (global N,
-all ranks; see ``executed_bytes``) / step time.  The default ``--mode dcgs2`` (CGS2 with delayed
-re-orthogonalisation) reads the basis 2x per Arnoldi step (``cgs2``: 3x), so it moves fewer bytes
-than SURVEY.md §8(d)'s 4-pass model
+all ranks; see ``executed_bytes``) / step time (max over ranks).  The default ``--mode dcgs2``
+(CGS2 with delayed re-orthogonalisation) reads the basis 2x per Arnoldi step (``cgs2``: 3x), so it
+moves fewer bytes than SURVEY.md §8(d)'s 4-pass model
   B(j) = 8 [2j(N_w+N) + 2(N_w+n_v) + 4N + n_v + 2N]  (+ 8*3N matvec);
 that model divided by the same time is reported separately as ``effective_gbs_survey_model`` (the
-work definition the CPU baseline is also measured in; it exceeds the HBM peak because the
-executed algorithm does half the model's reads).  ``roofline`` is the dominant kernel family
-(two-vector multi-dot, dual update, or the cgs2 kernels) timed live with HIP events on the launch
-stream.  ``restart`` (outside the timed region) times one Krylov–Schur condensation of the final
-factorisation: the kept-column rotation the solver runs (HBM-bound) and the reference's full
-k-column rotation (2Nk^2 flop, priced against the fp64 peak; f64 MFMA).
+work definition the CPU baseline is also reported in).  ``roofline`` is the dominant kernel family
+timed live with HIP events on the launch stream.  Outside the timed region: ``restart`` times one
+Krylov–Schur condensation of the final factorisation (H rescaled to unit spectral radius, see
+there), and ``krylov_schur_leg`` runs the config-3 operator through real Krylov–Schur restarts.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,16 +48,27 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 spec (vector = matrix on CDNA4); SURVEY.md §8(d) ridge ~10 flop/B
+N_HEADLINE = 100_014_464  # config 3, E=44,176
+
+
+# ---- byte models ---------------------------------------------------------------------------------
+
+def survey_step_bytes(N, N_w, n_v, j):
+    """SURVEY.md §8(d) B(j) of a 4-pass CGS2 step plus the matvec (8*3N)."""
+    return 8.0 * (2 * j * (N_w + N) + 2 * (N_w + n_v) + 4 * N + n_v + 2 * N) + 8.0 * 3 * N
 
 
 def survey_model_bytes(N, N_w, n_v, m):
-    """SURVEY.md §8(d) byte model of a 4-pass CGS2 step, Σ_j B(j), plus the matvec (8*3N per step).
-    Used for the CPU baseline and as the *effective* rate of the GPU (same work definition)."""
-    tot = 0.0
-    for j in range(1, m + 1):
-        tot += 8.0 * (2 * j * (N_w + N) + 2 * (N_w + n_v) + 4 * N + n_v + 2 * N)
-        tot += 8.0 * 3 * N
-    return tot
+    """Σ_j B(j) (+ matvec): the CPU baseline's work definition and the GPU's *effective* rate."""
+    return sum(survey_step_bytes(N, N_w, n_v, j) for j in range(1, m + 1))
+
+
+def reference_step_bytes(N, N_w, n_v, j):
+    """Bytes the reference's own MGS2 moves at step j (update_hessenberg_matrix,
+    krylov_decomposition.f90:152-186), per basis column and pass: k_copy 2N, k_dot 3N_w (p, w, q per
+    weighted field), k_cmult 2N, k_sub2 3N; plus the unused k_norm (:152, 3N_w), the closing
+    k_normalize (3N_w + 2N) and the matvec (3N).  ≈ 20jN per step."""
+    return 8.0 * (2 * j * (7 * N + 3 * N_w) + 6 * N_w + 2 * N + 3 * N)
 
 
 def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
@@ -76,6 +95,8 @@ def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
     return tot
 
 
+# ---- host CPU facts ----------------------------------------------------------------------------
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -86,10 +107,48 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float, variant: str = "mgs2"):
-    """The reference algorithm (MGS + full re-orthogonalisation with per-field weighted dots, copy
-    -> dot -> cmult -> sub2, krylov_decomposition.f90:155-180) restated in C (oracle/), on the same
-    operator family at a bounded sample size, timed on this host.  Steps run until ``budget_s``.
+def _cgroup_cpus():
+    """CPU quota of this process's cgroup in CPUs (v2 cpu.max or v1 cfs quota), None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
+def host_threads() -> dict:
+    """Threads the CPU baseline uses: every CPU this process may run on (sched_getaffinity),
+    capped by the cgroup quota and by the host's declared CPU share (OMP_NUM_THREADS: 16 per GPU
+    on the GPU boxes, whose nproc shows the whole machine).  All inputs are recorded."""
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = aff
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return dict(threads=n, affinity_cpus=aff, nproc=os.cpu_count(), cgroup_quota_cpus=quota,
+                omp_num_threads=omp, cpu=cpu_model())
+
+
+# ---- CPU baseline ------------------------------------------------------------------------------
+
+def cpu_baseline(E_sample: int, m: int, threads: int, js, variant: str = "mgs2", n_full: int = N_HEADLINE):
+    """The reference algorithm timed on this host: MGS + full re-orthogonalisation with per-field
+    weighted dots (copy -> dot -> cmult -> sub2, krylov_decomposition.f90:152-186), restated in C
+    (oracle/nekstab_oracle.c, built -Ofast like the reference's bin/mks:53-55), on the config-3
+    layout at ``E_sample`` elements.  The basis Q[0:max(js)] is pre-built (hashed vectors; MGS2's
+    cost does not depend on the values), then single Arnoldi steps j in ``js`` are timed (matvec +
+    update_hessenberg_matrix on a fresh f).  The per-step time is linear in j, t(j) = a + b j
+    (least squares over ``js``), so a full m-step factorisation costs Σ_j t(j); it is reported at
+    the sample size and scaled by N to BASELINE's N=1e8 (seconds to solution).
     ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
@@ -100,11 +159,7 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float, variant: 
 
     lay = box3d_layout(E_sample)
     L = orc.OLayout(lay.n_v, lay.n_p, lay.n_wf, False, lay.ldim)
-    w = syn.mass_weights(lay)
-    d, _ = syn.laplacian_shift_invert(lay)
-    dref = syn.to_reference_order(lay, d)
-    # the reference-order restatement timed as the reference is deployed (-Ofast, bin/mks:53-55);
-    # the strict-order build (liboracle.so) is the parity checker and ~2.5x slower per primitive
+    c = ctypes.byref(L.c)
     olib = orc.prod_lib()
     olib.orc_set_threads(threads)
     if variant == "cgs2":
@@ -112,35 +167,110 @@ def cpu_baseline(E_sample: int, m: int, threads: int, budget_s: float, variant: 
         step = orc.cgs2_lib().cpu_cgs2_update_hessenberg
     else:
         step = olib.orc_update_hessenberg
-    Q = np.zeros((m + 1, L.len))
-    Q[0] = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 11)))
-    f = L.zeros()
-    wrk = L.zeros()
-    c = ctypes.byref(L.c)
-    done_bytes, t0, steps = 0.0, time.perf_counter(), 0
-    for j in range(1, m + 1):
+    w = syn.mass_weights(lay)
+    d, _ = syn.laplacian_shift_invert(lay)
+    dref = syn.to_reference_order(lay, d)
+    del d
+    jmax = max(js)
+    Q = np.empty((jmax, L.len))
+    for i in range(jmax):
+        olib.orc_fill_hash(c, Q[i], 1000 + i, 0, 0)
+    f, wrk = L.zeros(), L.zeros()
+    t_step, t_mv = {}, []
+    for j in js:
+        t0 = time.perf_counter()
         olib.orc_op_diag(c, dref, Q[j - 1], f, 0.0)
+        t1 = time.perf_counter()
         col = np.zeros(j + 1)
-        step(c, w, col, f, Q[:j], j, wrk)  # Q rows are contiguous views
-        Q[j] = f
-        done_bytes += 8.0 * (2 * j * (lay.N_w + lay.N) + 2 * (lay.N_w + lay.n_v) + 4 * lay.N + lay.n_v + 2 * lay.N)
-        done_bytes += 8.0 * 3 * lay.N
-        steps = j
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
+        step(c, w, col, f, Q[:j], j, wrk)
+        t_step[j] = time.perf_counter() - t1
+        t_mv.append(t1 - t0)
     olib.orc_set_threads(1)
+    del Q
+    jj = np.array(sorted(t_step), dtype=np.float64)
+    tt = np.array([t_step[j] for j in sorted(t_step)])
+    if len(jj) > 1:
+        b, a = np.polyfit(jj, tt, 1)
+    else:
+        a, b = 0.0, tt[0] / jj[0]
+    mv = float(np.median(t_mv))
+    sec_fact = m * (a + mv) + b * m * (m + 1) / 2.0          # Σ_{j=1..m} [matvec + t(j)] at the sample N
+    scale = n_full / lay.N
+    surv = survey_model_bytes(lay.N, lay.N_w, lay.n_v, m)
+    refb = sum(reference_step_bytes(lay.N, lay.N_w, lay.n_v, j) for j in range(1, m + 1))
     what = ("reference MGS2 Arnoldi (C restatement oracle/nekstab_oracle.c, built -Ofast like the "
             "reference's bin/mks)" if variant == "mgs2" else
             "optimised CPU: blocked OpenMP CGS2 (oracle/cpu_cgs2.c, AVX2/FMA)")
-    return dict(value=done_bytes / dt / 1e9, unit="GB/s", cores=threads, kind="port",
-                sample=(f"{what} on the same 3-D lx1=8 layout at E={E_sample} (N={lay.N}), steps j=1..{steps} "
-                        f"of m={m}, {dt:.1f} s, {threads} thread(s) on {cpu_model()}; GB/s in SURVEY.md "
-                        f"§8(d)'s CGS2 byte model (compare with effective_gbs_survey_model)"),
-                seconds=dt)
+    return dict(
+        value=round(surv / sec_fact / 1e9, 2), unit="GB/s (SURVEY.md 8(d) model bytes)", cores=threads, kind="port",
+        value_reference_executed_gbs=round(refb / sec_fact / 1e9, 2) if variant == "mgs2" else None,
+        seconds_per_factorisation_sample=round(sec_fact, 3),
+        seconds_per_factorisation_N1e8=round(sec_fact * scale, 2),
+        step_seconds={int(j): round(t_step[j], 4) for j in sorted(t_step)},
+        fit_seconds={"a": float(a), "b_per_column": float(b), "matvec": mv},
+        sample=(f"{what}; config-3 layout (3-D lx1=8, {{vx,vy,vz,t}}+pr) at E={E_sample} (N={lay.N}); single "
+                f"Arnoldi steps j={list(map(int, jj))} timed on a pre-built basis, t(j)=a+b*j fitted, Σ_j over "
+                f"m={m}; seconds scaled by N to N={n_full}; {threads} thread(s) on {cpu_model()}"))
 
 
-def main():
+# ---- launcher ----------------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv, grace_s: float = 60.0) -> int:
+    """Spawn ``n`` ranks of this script (torch.distributed.run's environment, no exec) and return
+    the worst exit status.  If one rank fails, the others get ``grace_s`` to finish (a rank blocked
+    in a collective never does) and are then terminated."""
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NKV_BENCH_LAUNCHER="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+
+    def _stop(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, _stop) for s in (signal.SIGTERM, signal.SIGINT)}
+    rcs = [None] * n
+    t_fail = None
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rc = p.poll()
+                    if rc is not None:
+                        rcs[i] = rc
+                        if rc != 0 and t_fail is None:
+                            t_fail = time.monotonic()
+                            print(f"bench launcher: rank {i} exited with {rc}", file=sys.stderr, flush=True)
+            if t_fail is not None and time.monotonic() - t_fail > grace_s:
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        p.terminate()
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = p.wait(timeout=20)
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            rcs[i] = p.wait()
+            time.sleep(0.05)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    norm = [rc if rc >= 0 else 128 - rc for rc in rcs]   # killed by signal k -> 128 + k
+    return max(norm)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -150,14 +280,69 @@ def main():
     ap.add_argument("--mode", default="dcgs2", help="dcgs2 (default) | cgs2 | cgs2-unfused")
     ap.add_argument("--lazy-basis", action="store_true",
                     help="dcgs2 over a lazy basis Q = S T (one vector write less per step)")
-    ap.add_argument("--cpu-E", type=int, default=512)
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-E", type=int, default=11044, help="CPU baseline sample (11,044 -> N=2.5e7)")
+    ap.add_argument("--cpu-js", default="1,32,64,128", help="Arnoldi steps timed on the CPU (all threads)")
+    ap.add_argument("--cpu-js-1core", default="1,8", help="... with one thread")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-restart", action="store_true", help="skip the restart-rotation measurement")
+    ap.add_argument("--no-ks", action="store_true", help="skip the Krylov–Schur restart leg")
     ap.add_argument("--force-collectives", action="store_true",
                     help="at one GPU, route every partial through a world-1 RCCL group (collective cost)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="print each rank's launch environment and stop before GPU initialisation")
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse_args()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:], grace_s=float(os.environ.get("NKV_LAUNCH_GRACE_S", "60"))))
+    world_env = int(ws) if ws is not None else 1
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; refusing to run", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_launch:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        print(json.dumps({"dry_launch": True, "pid": os.getpid(), **{k: os.environ.get(k) for k in keys}}),
+              flush=True)
+        r = os.environ.get("RANK", "0")   # test hooks: a rank that hangs / fails
+        time.sleep(float(os.environ.get("NKV_DRY_SLEEP_RANK" + r, "0")))
+        sys.exit(int(os.environ.get("NKV_DRY_RC_RANK" + r, "0")))
+    run(args)
+
+
+# ---- one rank ----------------------------------------------------------------------------------
+
+def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed):
+    """BASELINE config 3's Krylov–Schur leg at full N with restarts that really happen: the
+    shift-invert operator scaled to unit spectral radius (|mu| / max|mu|, the spectrum a
+    time-stepper exp(L dt) would present), k_dim=12, schur_tgt=4, eigen_tol=1e-10.  The oracle runs
+    the same (schur_cnt 1, mstart [9]) at reduced N (tests/test_gpu_solvers.py)."""
+    import torch
+
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.krylov_schur import krylov_schur
+    from nekstab_next_amd.operators import DiagOperator
+
+    op = DiagOperator(ctx, d_scaled)
+    cfg = KrylovSchurConfig(k_dim=12, schur_tgt=4, eigen_tol=1e-10)
+    krylov_schur(ctx, op, seed, cfg, Q=Q)       # warm-up (first-touch of small buffers)
+    torch.cuda.synchronize(ctx.device)
+    ctx.comm.barrier()
+    t0 = time.perf_counter()
+    res = krylov_schur(ctx, op, seed, cfg, Q=Q)
+    torch.cuda.synchronize(ctx.device)
+    dt = ctx.comm.max_scalar(time.perf_counter() - t0, device=ctx.device)
+    conv = res.residual < cfg.eigen_tol
+    errs = [float(np.min(np.abs(exact_scaled - v)) / abs(v)) for v in res.vals[conv]]
+    return {"k_dim": 12, "schur_tgt": 4, "eigen_tol": 1e-10, "operator": "config-3 shift-invert / max|mu|",
+            "seconds": round(dt, 4), "schur_cnt": int(res.schur_cnt), "mstart_history": list(map(int, res.mstart_history)),
+            "cnt_history": list(map(int, res.cnt_history)), "converged": int(res.converged),
+            "ritz_rel_err_vs_exact": max(errs) if errs else None}
+
+
+def run(args):
     import torch
 
     from nekstab_next_amd import lapack
@@ -171,11 +356,16 @@ def main():
     from nekstab_next_amd.profiling import PhaseTimer
     from nekstab_next_amd.vector import NekContext
 
-    comm = init_from_env(os.environ.get("NKV_BACKEND", "nccl"), force_collectives=args.force_collectives)
+    backend = os.environ.get("NKV_BACKEND", "nccl")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world_env > max(1, ndev):
+        print(f"bench.py: {world_env} RCCL ranks need {world_env} GPUs, {ndev} visible "
+              f"(NKV_BACKEND=gloo shares one GPU between ranks)", file=sys.stderr)
+        sys.exit(2)
+    comm = init_from_env(backend, force_collectives=args.force_collectives)
     rank, world = comm.rank, comm.world
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -186,6 +376,8 @@ def main():
     ctx = NekContext(lay, weights=w, comm=comm, max_cols=m + 1, device=dev)
     d, exact = syn.laplacian_shift_invert(lay)
     op = DiagOperator(ctx, d)
+    rho = float(np.abs(exact[0]))
+    d_scaled = d / rho
     del d
     seed = ctx.vector()
     seed.fill_hash(11)
@@ -207,6 +399,7 @@ def main():
         one_step()
     timer = PhaseTimer(dev)
     ctx.timer = timer
+    comm.timer = timer
     comm.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -217,6 +410,7 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_scalar(elapsed, device=dev)
     ctx.timer = None
+    comm.timer = None
     phases = timer.summary()
     last_step_ms = sum(timer.last_ms(k) for k in ("block_dot2", "dcgs2_update")) if args.mode == "dcgs2" else None
     ctx.check_nan()
@@ -229,7 +423,7 @@ def main():
         rt = PhaseTimer(dev)
         ctx.timer = rt
         # the shift-invert spectrum is not inside the unit disc (every |mu| >= 1 - schur_del would be
-        # kept); scale H by its spectral radius as a time-stepper's exp(L dt) spectrum would be —
+        # kept); H is divided by its spectral radius as a time-stepper's exp(L dt) spectrum would be —
         # same Schur vectors, the selection rule then keeps the leading cluster + nev + 4
         H = Hd.download()
         H /= np.max(np.abs(vals))
@@ -248,12 +442,20 @@ def main():
         kept, full = rp["rotate"], rp["rotate_full"]
         full_tf = 2.0 * lay.N * m * m / (full["avg_ms"] * 1e-3) / 1e12
         restart = {
+            "note": ("one condensation of the timed run's final factorisation with H divided by its spectral "
+                     "radius (synthetic: the raw shift-invert spectrum lies outside the unit disc, so the "
+                     "selection rule would keep every column); rotate_full is the reference's full k-column "
+                     "Q V on a random orthogonal V"),
             "mstart": int(mstart), "condensation_wall_ms": round(cond_ms, 2),
             "rotate_kept_ms": round(kept["avg_ms"], 3), "rotate_kept_gbs": round(kept["gbps"], 1),
             "rotate_kept_frac_hbm": round(kept["gbps"] / HBM_PEAK_GBS, 4),
             "rotate_full_ms": round(full["avg_ms"], 3), "rotate_full_tflops": round(full_tf, 2),
             "rotate_full_frac_fp64": round(full_tf / FP64_PEAK_TFLOPS, 4),
         }
+    ks_leg = None
+    if not args.no_ks:
+        ks_leg = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed)
+    del d_scaled
 
     ms_per_step = elapsed / args.steps * 1e3
     nv_g = glay.pts_v * glay.nelgv
@@ -264,15 +466,28 @@ def main():
     # and launch gaps excluded; kernel-bracketed HIP events, this rank), and the last step alone
     gs_fams = ("block_dot", "update_dot", "block_update", "finish", "block_dot2", "dcgs2_update")
     gs_ms = sum(phases[k]["total_ms"] for k in gs_fams if k in phases) / args.steps
+    ar = phases.get("allreduce")
+    ar_ms = (ar["total_ms"] / args.steps) if ar else 0.0
     gs_exec = sum(phases[k]["avg_bytes"] * phases[k]["launches"] for k in gs_fams if k in phases) / args.steps
     survey_gs = survey_model_bytes(lay.N, lay.N_w, lay.n_v, m) - m * 8.0 * 3 * lay.N
     b_last = 8.0 * (2 * m * (lay.N_w + lay.N) + 2 * (lay.N_w + lay.n_v) + 4 * lay.N + lay.n_v + 2 * lay.N)
+    gs_min, gs_max = comm.min_scalar(gs_ms, device=dev), comm.max_scalar(gs_ms, device=dev)
+    ar_min, ar_max = comm.min_scalar(ar_ms, device=dev), comm.max_scalar(ar_ms, device=dev)
     gs = {"gs_ms_per_factorisation": round(gs_ms, 2),
+          "gs_ms_per_factorisation_min_over_ranks": round(gs_min, 2),
+          "gs_ms_per_factorisation_max_over_ranks": round(gs_max, 2),
+          "allreduce_ms_per_factorisation": round(ar_ms, 3),
+          "allreduce_ms_per_factorisation_min_over_ranks": round(ar_min, 3),
+          "allreduce_ms_per_factorisation_max_over_ranks": round(ar_max, 3),
+          "allreduces_per_factorisation": (ar["launches"] // args.steps) if ar else 0,
+          "gs_incl_allreduce_ms": round(gs_ms + ar_ms, 2),
           "executed_gs_gbs": round(gs_exec / (gs_ms * 1e-3) / 1e9, 1),
           "survey_headline_gbs": round(survey_gs / (gs_ms * 1e-3) / 1e9, 1),
           "last_step_ms": None if last_step_ms is None else round(last_step_ms, 3),
           "last_step_survey_gbs": None if last_step_ms is None else round(b_last / (last_step_ms * 1e-3) / 1e9, 1),
-          "note": "per rank; survey_* use SURVEY.md 8(d)'s 4-pass CGS2 byte model B(j) for the same work"}
+          "note": ("rank-0 shard unless *_over_ranks; events on the launch stream; allreduce = events around "
+                   "torch.distributed.all_reduce of the step's partial vector (0 at world 1); survey_* use "
+                   "SURVEY.md 8(d)'s 4-pass CGS2 byte model B(j) for the same work")}
 
     # Ritz accuracy vs the exact spectrum of the synthetic operator
     # (exact spectrum: the 4096 largest |mu|; a converged Ritz value is matched to the nearest one)
@@ -286,28 +501,42 @@ def main():
               key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
     ph = phases[dom]
     achieved = ph["gbps"]
-    traffic = None
+    traffic, tsrc = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get("kernel_family") == dom and tj.get("E") == args.E and tj.get("m") == m and world == 1:
                 traffic = tj.get("hbm_bytes_per_launch")
+                tsrc = {"file": "profiles/traffic_latest.json", "collected": tj.get("source"),
+                        "box": tj.get("box"), "head": tj.get("head"),
+                        "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate "
+                                  "passes, tools/pmc_traffic.py; not collected in this run"}
         except Exception:  # noqa: BLE001
             traffic = None
 
     if rank == 0:
-        cpu = cpu1 = cpu_opt = None
+        cpu = cpu1 = cpu_opt = host = None
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)   # the box's CPU share is 16 cores
-            cpu = cpu_baseline(args.cpu_E, m, threads, args.cpu_budget)
-            cpu1 = cpu_baseline(args.cpu_E, m, 1, args.cpu_budget / 2)
-            cpu_opt = cpu_baseline(args.cpu_E, m, threads, args.cpu_budget / 2, variant="cgs2")
+            host = host_threads()
+            js = [int(x) for x in args.cpu_js.split(",")]
+            js1 = [int(x) for x in args.cpu_js_1core.split(",")]
+            cpu = cpu_baseline(args.cpu_E, m, host["threads"], js)
+            cpu1 = cpu_baseline(args.cpu_E, m, 1, js1)
+            cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], js, variant="cgs2")
+            for c in (cpu, cpu1, cpu_opt):
+                c["gpu_ms_per_factorisation"] = round(ms_per_step, 2)
+                c["gpu_effective_gbs_same_model"] = round(effective, 2)
+                c["time_to_solution_ratio_cpu_over_gpu"] = round(c["seconds_per_factorisation_N1e8"] /
+                                                                 (ms_per_step * 1e-3), 1)
+            cpu["host"] = host
         out = {
             "metric": "Arnoldi-step GB/s (achieved HBM) + Ritz-value rel-err, N=1e8 m=128",
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
+            "world": world,
+            "backend": comm.backend if world > 1 or args.force_collectives else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -320,7 +549,8 @@ def main():
             "config": {
                 "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
                 "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
-                "m": m, "mode": args.mode + ("-lazy" if lazy else ""), "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
+                "m": m, "mode": args.mode + ("-lazy" if lazy else ""),
+                "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
                                 + " allreduce") if world > 1 else "single GPU",
             },
             "roofline": {
@@ -331,6 +561,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": tsrc,
                 "avg_launch_ms": round(ph["avg_ms"], 4),
                 "avg_bytes_per_launch": ph["avg_bytes"],
                 "launches": ph["launches"],
@@ -341,10 +572,11 @@ def main():
             "ritz_rel_err": ritz_err,
             "ritz_top8_rel_err": top_err,
             "ritz_converged": int(conv.sum()),
-            "cpu_baseline": ({k: v for k, v in cpu.items() if k != "seconds"} if cpu else None),
-            "cpu_baseline_1core": ({k: v for k, v in cpu1.items() if k != "seconds"} if cpu1 else None),
-            "cpu_optimised": ({k: v for k, v in cpu_opt.items() if k != "seconds"} if cpu_opt else None),
+            "cpu_baseline": cpu,
+            "cpu_baseline_1core": cpu1,
+            "cpu_optimised": cpu_opt,
             "restart": restart,
+            "krylov_schur_leg": ks_leg,
         }
         print(json.dumps(out), flush=True)
     comm.barrier()

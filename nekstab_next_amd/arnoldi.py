@@ -309,7 +309,7 @@ class FactorizationGraph:
     Every launch of a factorisation (matvec kernels, the Gram–Schmidt kernels, the RCCL all-reduces
     when the process group is ``nccl``) is captured once per (mstart, mend, transpose) into a
     ``torch.cuda.CUDAGraph`` on the compute stream and replayed: no host work and no launch
-    latency between kernels.  All buffers (basis, H, f, workspace, partial vectors) are allocated
+    latency between kernels.  World size 1 only (see ``usable``).  All buffers (basis, H, f, workspace, partial vectors) are allocated
     before capture and never move.  The operator must be capturable (device kernels only: no host
     synchronisation in ``matvec``); a ``gloo`` group (host all-reduce) cannot be captured, so
     ``usable()`` is False for it and callers fall back to eager launches."""
@@ -321,7 +321,11 @@ class FactorizationGraph:
         self.graphs = {}
 
     def usable(self) -> bool:
-        return self.ctx.comm.world == 1 or self.ctx.comm.backend == "nccl"
+        """Single rank only.  Capturing RCCL all-reduces into a replayed graph has never run on more
+        than one GPU (round 1 rehearsed world > 1 only as gloo ranks sharing one GPU), so a
+        multi-rank factorisation always launches eagerly; ``krylov_schur`` refuses
+        ``graphs=True`` at world > 1 instead of silently falling back."""
+        return self.ctx.comm.world == 1
 
     def run(self, mstart: int, mend: int, transpose: bool = False) -> None:
         if mend < mstart:

@@ -19,6 +19,7 @@ class Comm:
 
     def __init__(self, group=None, force_collectives: bool = False):
         self.group = group
+        self.timer = None   # optional profiling.PhaseTimer: events around every all-reduce (bench.py)
         # force_collectives: issue the all-reduces even at world size 1 (an initialised world-1
         # group) — measures the collective path's cost without peers (bench.py --force-collectives)
         self.force = bool(force_collectives) and dist.is_available() and dist.is_initialized()
@@ -37,12 +38,20 @@ class Comm:
         """In-place SUM all-reduce of a device partial (deterministic: RCCL gives every rank the
         same bits, so host LAPACK stays replicated on identical data)."""
         if self.world > 1 or self.force:
+            tm = self.timer
+            if tm is not None:
+                tm.begin("allreduce")
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            if tm is not None:
+                tm.end("allreduce", 8.0 * t.numel())
         return t
 
     def barrier(self) -> None:
         if self.world > 1:
             dist.barrier(group=self.group)
+
+    def min_scalar(self, x: float, device=None) -> float:
+        return -self.max_scalar(-x, device=device)
 
     def max_scalar(self, x: float, device=None) -> float:
         if self.world == 1 and not self.force:

@@ -131,6 +131,9 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
     hook = None if on_step is None else (lambda mstep: on_step(mstep, Q, Hd))
     lazy = cfg.lazy_basis and cfg.mode == "dcgs2" and hook is None
+    if cfg.graphs and ctx.comm.world > 1:
+        raise ValueError("KrylovSchurConfig.graphs=True is refused at world size > 1: HIP-graph capture of "
+                         "the RCCL all-reduces has not been validated on more than one GPU; run eagerly")
     graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode, lazy) if (cfg.graphs and hook is None) else None
     if graphs is not None and not graphs.usable():
         graphs = None

@@ -214,11 +214,14 @@ static inline uint64_t mix64(uint64_t z) {
 
 void orc_fill_hash(const orc_layout* L, double* x, uint64_t seed, int64_t voff, int64_t poff) {
     const uint64_t key0 = seed * 0xD1342543DE82EF95ull;
+    /* every element is a pure function of its index: threads change nothing but the speed */
     for (int f = 0; f < L->nwf; ++f)
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
         for (int64_t i = 0; i < L->nv; ++i) {
             const uint64_t z = mix64(key0 + (uint64_t)f * 0x9E3779B97F4A7C15ull + (uint64_t)(voff + i));
             x[(int64_t)f * L->nv + i] = 2.0 * ((double)(z >> 11) * 0x1.0p-53) - 1.0;
         }
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
     for (int64_t i = 0; i < L->np; ++i) {
         const uint64_t z = mix64(key0 + 31ull * 0x9E3779B97F4A7C15ull + (uint64_t)(poff + i));
         x[(int64_t)L->nwf * L->nv + i] = 2.0 * ((double)(z >> 11) * 0x1.0p-53) - 1.0;

@@ -50,8 +50,43 @@ def test_bench_cpu_baseline_leg_small():
     import bench
 
     for variant in ("mgs2", "cgs2"):
-        r = bench.cpu_baseline(8, 6, 2, 5.0, variant=variant)
+        r = bench.cpu_baseline(8, 6, 2, [1, 3, 6], variant=variant)
         assert {"value", "unit", "cores", "kind", "sample"} <= set(r)
-        assert r["unit"] == "GB/s" and r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
-        assert "steps j=1..6 of m=6" in r["sample"]
-    assert "-Ofast" in bench.cpu_baseline(8, 4, 1, 5.0)["sample"]
+        assert r["unit"].startswith("GB/s") and r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+        assert "j=[1, 3, 6]" in r["sample"] and "m=6" in r["sample"]
+    assert "-Ofast" in bench.cpu_baseline(8, 4, 1, [1, 2])["sample"]
+
+
+def test_bench_cpu_baseline_sampled_and_extrapolated():
+    """bench.cpu_baseline times single steps on a pre-built basis, fits t(j) = a + b j and reports
+    both byte models and seconds to solution scaled to N=1e8."""
+    import bench
+
+    r = bench.cpu_baseline(16, 16, 2, [1, 4, 8])
+    assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+    assert r["value_reference_executed_gbs"] > r["value"]        # the reference moves ~5x the model's bytes
+    assert sorted(r["step_seconds"]) == [1, 4, 8]
+    lay_N = box3d_layout(16).N
+    assert abs(r["seconds_per_factorisation_N1e8"] / r["seconds_per_factorisation_sample"]
+               - bench.N_HEADLINE / lay_N) < 0.05 * bench.N_HEADLINE / lay_N
+    o = bench.cpu_baseline(16, 16, 2, [1, 8], variant="cgs2")
+    assert o["value"] > 0 and o["value_reference_executed_gbs"] is None
+
+
+def test_host_threads_respects_cpu_share(monkeypatch):
+    import bench
+
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    h = bench.host_threads()
+    assert h["threads"] == min(3, h["affinity_cpus"]) and h["nproc"] >= 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    h = bench.host_threads()
+    assert 1 <= h["threads"] <= h["affinity_cpus"]
+
+
+def test_reference_byte_model_is_about_20jN():
+    import bench
+
+    N, N_w, n_v = 100_014_464, 90_472_448, 22_618_112
+    per_col = (bench.reference_step_bytes(N, N_w, n_v, 101) - bench.reference_step_bytes(N, N_w, n_v, 100)) / 8
+    assert 18 * N < per_col < 21 * N

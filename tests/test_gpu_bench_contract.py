@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_json_contract(gpu):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--E", "2000", "--steps", "2", "--warmup", "1",
-                        "--cpu-E", "64", "--cpu-budget", "1.0"], capture_output=True, text=True, timeout=240,
+                        "--cpu-E", "64", "--cpu-js", "1,4,8", "--cpu-js-1core", "1,2"],
+                       capture_output=True, text=True, timeout=240,
                        cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -30,6 +31,34 @@ def test_bench_json_contract(gpu):
     assert r["bound"] == "hbm" and r["peak"] == 8000.0 and r["unit"] == "GB/s"
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     cb = d["cpu_baseline"]
-    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"] == "GB/s"
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
+    assert cb["cores"] == cb["host"]["threads"] and cb["seconds_per_factorisation_N1e8"] > 0
+    assert cb["value_reference_executed_gbs"] > cb["value"]
+    assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
+    ks = d["krylov_schur_leg"]
+    assert ks["schur_cnt"] >= 1 and ks["converged"] >= 4 and ks["ritz_rel_err_vs_exact"] < 1e-10
     assert d["ritz_top8_rel_err"] < 1e-10
     assert d["gram_schmidt"]["gs_ms_per_factorisation"] <= d["ms_per_step"]
+
+
+def test_bench_plain_command_two_gloo_ranks_one_gpu(gpu):
+    """``python bench.py --gpus 2`` (no torchrun) spawns two ranks; with NKV_BACKEND=gloo both share
+    the one GPU of this box.  One JSON line with n_gpus 2, and the same Ritz values as one rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["NKV_BACKEND"] = "gloo"
+    common = ["--E", "2000", "--m", "48", "--steps", "1", "--warmup", "1", "--no-cpu", "--no-restart", "--no-ks"]
+    outs = {}
+    for n in (1, 2):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *common],
+                           capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+        assert p.returncode == 0, p.stderr[-3000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, p.stdout
+        outs[n] = json.loads(lines[0])
+    d2 = outs[2]
+    assert d2["n_gpus"] == 2 and d2["world"] == 2 and d2["backend"] == "gloo"
+    g = d2["gram_schmidt"]
+    assert g["allreduces_per_factorisation"] >= 48 and g["allreduce_ms_per_factorisation_max_over_ranks"] > 0
+    assert g["gs_ms_per_factorisation_min_over_ranks"] <= g["gs_ms_per_factorisation_max_over_ranks"]
+    assert abs(d2["ritz_top8_rel_err"] - outs[1]["ritz_top8_rel_err"]) < 1e-12
+    assert d2["ritz_converged"] == outs[1]["ritz_converged"]
