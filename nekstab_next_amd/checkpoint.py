@@ -39,17 +39,38 @@ def write_hes(path: str, H: np.ndarray, k: int) -> None:
                 fh.write(f"{H[i, j]: .17E}\n")
 
 
+def _list_directed_reals(text: str, count: int, path: str) -> np.ndarray:
+    """The first ``count`` items of a Fortran list-directed real read: blank / comma / newline
+    separators, ``r*c`` repeat counts, D exponents."""
+    vals = []
+    for tok in text.replace(",", " ").split():
+        if "*" in tok:
+            r, c = tok.split("*", 1)
+            vals.extend([float(c.replace("D", "E").replace("d", "e"))] * int(r))
+        else:
+            vals.append(float(tok.replace("D", "E").replace("d", "e")))
+        if len(vals) >= count:
+            break
+    if len(vals) < count:
+        raise ValueError(f"{path}: {len(vals)} values, {count} expected")
+    return np.array(vals[:count], dtype=np.float64)
+
+
 def read_hes(path: str, mstart: int, k_dim: int) -> np.ndarray:
-    """H (k_dim+1, k_dim) with rows 1..mstart+1, cols 1..mstart filled, read row-major
-    (eigensolvers.f90:262; whitespace/list-directed, also the (1E15.7) one-per-line variant)."""
-    vals = np.array(open(path).read().split(), dtype=np.float64)
-    H = np.zeros((k_dim + 1, k_dim), order="F")
-    m = min(mstart, k_dim)
+    """H (k_dim+1, k_dim) with rows 1..mstart+1, cols 1..mstart filled, read row-major as the
+    reference's list-directed ``read (67, *) ((H(i, j), j=1, mstart), i=1, mstart+1)``
+    (eigensolvers.f90:262).  ``mstart > k_dim`` is refused: the reference's "subsampling" branch
+    (:250-256) reads one (1E15.7) field per record, which takes the first value of each line of the
+    several-values-per-record file ``arnoldi_checkpoint`` writes (:837) — not a restatable restart."""
+    if mstart > k_dim:
+        raise ValueError(f"restart from HES at mstart={mstart} > k_dim={k_dim} is not supported "
+                         f"(the reference's subsampling read, eigensolvers.f90:250-256)")
+    if mstart < 1:
+        raise ValueError(f"mstart={mstart} < 1")
     need = (mstart + 1) * mstart
-    if vals.size < need:
-        raise ValueError(f"{path}: {vals.size} values, {need} expected")
-    A = vals[:need].reshape(mstart + 1, mstart)
-    H[: min(mstart + 1, k_dim + 1), :m] = A[: k_dim + 1, :m]
+    A = _list_directed_reals(open(path).read(), need, path).reshape(mstart + 1, mstart)
+    H = np.zeros((k_dim + 1, k_dim), order="F")
+    H[: mstart + 1, :mstart] = A
     return H
 
 

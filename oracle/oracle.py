@@ -296,16 +296,37 @@ def schur_condensation(L: OLayout, H, Q, k, schur_del, schur_tgt):
     return mstart, selected
 
 
-def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, schur_del=0.1, max_restarts=1000):
+def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, schur_del=0.1, max_restarts=1000,
+                 on_step=None, start=None, stop_after=None):
     """eigensolvers.f90:120-359 from a given first Krylov vector q1 (already normalised by the
-    caller as prepare_seed does, linear_stab.f90:287-291)."""
+    caller as prepare_seed does, linear_stab.f90:287-291).
+
+    ``on_step(k, Q, H)``: called after Arnoldi step k (``if (ifres) call arnoldi_checkpoint``,
+    krylov_decomposition.f90:84; nekio.checkpoint_writer).  ``start=(mstart, H, Qs)``: the restart
+    branch (``uparam(2) = mstart > 0``, eigensolvers.f90:240-285): H and Q(1..mstart+1) as read from
+    the files, then ``mstart = mstart + 1`` (:281) and the factorisation continues; ``q1`` is then
+    ignored.  ``stop_after``: end the run after that Arnoldi step (a job killed mid-run)."""
     Q = np.zeros((k_dim + 1, L.len))
     H = np.zeros((k_dim + 1, k_dim))
-    Q[0] = q1
     mstart, schur_cnt = 1, 0
+    if start is None:
+        Q[0] = q1
+    else:
+        ms, H0, Qs = start
+        H[...] = H0
+        Q[: ms + 1] = Qs[: ms + 1]
+        mstart = ms + 1
     hist = dict(mstart=[], cnt=[], selected=[], H_first=None)
     while True:
-        arnoldi_factorization(L, w, matvec, Q, H, mstart, k_dim)
+        if on_step is None and stop_after is None:
+            arnoldi_factorization(L, w, matvec, Q, H, mstart, k_dim)
+        else:
+            for mstep in range(mstart, k_dim + 1):
+                arnoldi_factorization(L, w, matvec, Q, H, mstep, mstep)
+                if on_step is not None:
+                    on_step(mstep, Q, H)
+                if stop_after is not None and mstep >= stop_after:
+                    return dict(stopped_at=mstep, Q=Q, H=H)
         if hist["H_first"] is None:
             hist["H_first"] = H.copy()
         vals, vecs = eig(H[:k_dim, :k_dim])
@@ -319,6 +340,40 @@ def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, sc
         hist["mstart"].append(mstart)
         hist["selected"].append(sel)
     return dict(vals=vals, vecs=vecs, residual=residual, converged=cnt, schur_cnt=schur_cnt, H=H, Q=Q, **hist)
+
+
+def outpost_mode(L: OLayout, w, Q, vecs, i, k):
+    """Eigenmode i as outpost_ks assembles it (eigensolvers.f90:565-585, 603-613):
+    ``fp = matmul(q(:, 1:k), vecs(:, i))`` field by field in complex arithmetic — with a real basis
+    the real and imaginary parts are the two real combinations Q y_re and Q y_im, summed over the
+    columns in ascending order (k_matmul's order); ``norm`` of each part (sqrt of
+    ``inner_product``: glsc3 with bm1s over vx, vy, [vz], t — pressure not dotted, :2-75);
+    beta = 1/sqrt(alpha_r^2 + alpha_i^2) applied by ``nopcmult`` to every field incl. pressure.
+    Returns (re, im, alpha_r, alpha_i) in reference order; the time slot stays 0 (a mode carries
+    no time component)."""
+    c = ctypes.byref(L.c)
+    Qk = np.ascontiguousarray(Q[:k])
+    re, im = L.zeros(), L.zeros()
+    lib().orc_k_matmul(c, re, Qk, np.ascontiguousarray(vecs[:k, i].real), k)
+    lib().orc_k_matmul(c, im, Qk, np.ascontiguousarray(vecs[:k, i].imag), k)
+    re[-1] = im[-1] = 0.0
+    nt = OLayout(L.nv, L.np, L.nwf, False, L.ldim)   # inner_product never includes time
+    ar = float(np.sqrt(k_dot(nt, w, re, re)))
+    ai = float(np.sqrt(k_dot(nt, w, im, im)))
+    beta = 1.0 / np.sqrt(ar ** 2 + ai ** 2)
+    lib().orc_k_cmult(c, re, beta)
+    lib().orc_k_cmult(c, im, beta)
+    re[-1] = im[-1] = 0.0
+    return re, im, ar, ai
+
+
+def get_vec(L: OLayout, Q, coeffs, k):
+    """LightKrylov ``get_vec(vec, X(1:k), coeffs)`` as nekStab calls it (linear_stab.f90:362,372):
+    vec = X(1:k) coeffs, real coefficients, the fields only (k_matmul order); time slot 0."""
+    out = L.zeros()
+    lib().orc_k_matmul(ctypes.byref(L.c), out, np.ascontiguousarray(Q[:k]), np.ascontiguousarray(coeffs[:k]), k)
+    out[-1] = 0.0
+    return out
 
 
 def prepare_seed(L: OLayout, w, seed):
