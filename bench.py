@@ -508,7 +508,7 @@ def run(args):
             tj = json.load(open(tpath))
             if tj.get("kernel_family") == dom and tj.get("E") == args.E and tj.get("m") == m and world == 1:
                 traffic = tj.get("hbm_bytes_per_launch")
-                tsrc = {"file": "profiles/traffic_latest.json", "collected": tj.get("source"),
+                tsrc = {"file": "profiles/traffic_latest.json", "collected": tj.get("tag") or tj.get("source"),
                         "box": tj.get("box"), "head": tj.get("head"),
                         "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate "
                                   "passes, tools/pmc_traffic.py; not collected in this run"}

@@ -7,7 +7,7 @@ FETCH_SIZE reports exactly half of a wide (16 B/lane) coalesced streaming read, 
 (all our streaming loads are 16 B/lane double2 loads; the copy kernel k_blas1<COPY> calibrates it:
 N*8 bytes read -> FETCH_SIZE*2*1024); WRITE_SIZE is exact for 16 B/lane stores.
 
-usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON
+usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON [--tag T --head H --box B]
 """
 import collections
 import csv
@@ -47,6 +47,7 @@ def fam_of(name):
 
 def main():
     fdir, wdir, bench_json, out_json = sys.argv[1:5]
+    opt = dict(zip(sys.argv[5::2], sys.argv[6::2]))
     F, W = load(fdir), load(wdir)
     bench = json.load(open(bench_json))
     agg = {}
@@ -64,7 +65,8 @@ def main():
                hbm_bytes_per_launch=agg.get(dom, {}).get("hbm_bytes_per_launch"),
                algorithmic_bytes_per_launch=bench["roofline"]["avg_bytes_per_launch"],
                families=agg, correction="FETCH_SIZE x2 (16 B/lane streaming reads on gfx950), KiB -> bytes",
-               source=[fdir, wdir])
+               source=[os.path.relpath(fdir), os.path.relpath(wdir)], tag=opt.get("--tag"),
+               head=opt.get("--head"), box=opt.get("--box"))
     json.dump(rec, open(out_json, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
