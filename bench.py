@@ -562,6 +562,8 @@ def run(args):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": tsrc,
+                "launch": ("one entry-point call per Arnoldi step (nkv_dcgs2_update: NKV_DC_ROUNDS row-band "
+                           "dispatches; events span all of them)" if dom == "dcgs2_update" else "one entry-point call"),
                 "avg_launch_ms": round(ph["avg_ms"], 4),
                 "avg_bytes_per_launch": ph["avg_bytes"],
                 "launches": ph["launches"],

@@ -428,6 +428,14 @@ def test_empty_shard(gpu):
     ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, 3, ctx.coef.data_ptr(), Q.col_ptr(3), f.ptr, Q.col_ptr(4),
              None, ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
     assert Q[3].time == t0
+    # the banded launches (NKV_DC_ROUNDS) still run once on an empty shard: the replicated time slot
+    # follows the update (s = 2: qbar.time = 2 u.time, f.time = 2 (A u).time)
+    coef[2 * 3 + 4] = 2.0
+    ctx.coef[: coef.size].copy_(torch.as_tensor(coef))
+    Q[3].time, f.time, Q[4].time = 0.25, 0.5, 9.0
+    ctx.call("nkv_dcgs2_update", ctx.w.data_ptr(), Q.ptr, 3, ctx.coef.data_ptr(), Q.col_ptr(3), f.ptr, Q.col_ptr(4),
+             None, ctx.ws.data_ptr(), NKV_TIME, ctx.stream)
+    assert Q[3].time == 0.5 and Q[4].time == 1.0
     torch.cuda.synchronize()
 
 

@@ -1,3 +1,9 @@
+// EXPERIMENT COPY of nekstab_next_amd/csrc/nekkrylov.hip — built only by tools/tune_kernels.py
+// (variants with "src": "exp"), never by build(); the product never loads it.
+// Round-2 experiments (the dual-update row bands, NKVX_CHUNKS/NKVX_ROUNDS and the multi-dot bands
+// NKVX_D2_CHUNKS, are logged in profiles/r02e-g_tune_*; the update bands went into the product as
+// NKV_DC_ROUNDS):
+//   NKVX_OPD_ROUNDS=R  the synthetic diagonal matvec as one launch per R grid-stride rounds.
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
 // Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
@@ -67,9 +73,6 @@ namespace {
 #define NKV_DC_ROUNDS 2  // DCGS2 updates: one launch per this many grid-stride rounds of row tiles (a
                          // "row band"); the launch boundaries keep the grid's loads and stores in one
                          // band: +9-19 % at N=1e8, +0-1 % at the 8-GPU shard (profiles/r02f_tune_*)
-#endif
-#ifndef NKV_STREAM_ROUNDS
-#define NKV_STREAM_ROUNDS 2  // synthetic diagonal matvec: one launch per this many grid-stride rounds
 #endif
 #ifndef NKV_D2_MAXB
 #define NKV_D2_MAXB 256  // workgroups of the two-vector multi-dot: one per CU (+1 % over 1024 at
@@ -1384,9 +1387,11 @@ __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q,
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__ d,
                                                       const double* __restrict__ x,
-                                                      double* __restrict__ y, int64_t time_off, double ts,
-                                                      int64_t c_lo, int64_t c_hi) {
-    for (int64_t ci = c_lo + blockIdx.x; ci < c_hi; ci += gridDim.x) {   // this launch's row band
+                                                      double* __restrict__ y, int64_t rows,
+                                                      int64_t time_off, double ts, int64_t c_lo = 0,
+                                                      int64_t c_hi = -1) {
+    const int64_t chunks = c_hi < 0 ? rows / (2 * kThreads * kStreamUnr) : c_hi;
+    for (int64_t ci = c_lo + blockIdx.x; ci < chunks; ci += gridDim.x) {
         const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
         double2 dv[kStreamUnr], xv[kStreamUnr];
 #pragma unroll
@@ -1398,7 +1403,7 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
         for (int u = 0; u < kStreamUnr; ++u)
             st2p(y, 2 * (p0 + u * kThreads), make_double2(dv[u].x * xv[u].x, dv[u].y * xv[u].y));
     }
-    if (c_lo == 0 && blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
+    if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
 }
 
 __global__ __launch_bounds__(kThreads) void k_op_rot2(const double* __restrict__ cs,
@@ -1886,12 +1891,10 @@ int nkv_dcgs2_update_lazy(const nkv_layout* L, const double* S_cols, int m, cons
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     auto kern = large ? k_dcgs2_lazy_update<NKV_DC_PAIRS> : k_dcgs2_lazy_update<NKV_PAIRS_SMALL>;
     const int band = band_tiles(tiles_total, g);
-    // one launch per row band (NKV_DC_ROUNDS); at least one, which also updates the time slot
-    for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {
+    for (int lo = 0; lo < tiles_total; lo += band) {   // one launch per row band (NKV_DC_ROUNDS)
         const int hi = lo + band < tiles_total ? lo + band : tiles_total;
-        const int gb = g < hi - lo ? g : (hi - lo > 0 ? hi - lo : 1);
-        hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, S_cols, L->ld, m, coef_dev, win, fout, lo, hi,
-                           rows_of(L), lo == 0 ? dt : 0);
+        hipLaunchKernelGGL(kern, dim3(g < hi - lo ? g : hi - lo), dim3(kThreads), 0, st, S_cols, L->ld, m, coef_dev,
+                           win, fout, lo, hi, rows_of(L), lo == 0 ? dt : 0);
         NKV_LAUNCHED();
     }
     return NKV_OK;
@@ -1928,11 +1931,10 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
         // one launch per row band of NKV_DC_ROUNDS grid-stride rounds: every launch boundary is a
         // grid-wide point where all loads and stores of the band have retired (no in-kernel barrier)
         const int band = band_tiles(tiles_total, g);
-        for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {   // >= 1 launch: also the time slot
+        for (int lo = 0; lo < tiles_total; lo += band) {
             const int hi = lo + band < tiles_total ? lo + band : tiles_total;
-            const int gb = g < hi - lo ? g : (hi - lo > 0 ? hi - lo : 1);
-            hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj, win, fout, w, L->sv,
-                               tpf, tiles_w, tiles_total, T, lo == 0 ? dt : 0, part, lo, hi);
+            hipLaunchKernelGGL(kern, dim3(g < hi - lo ? g : hi - lo), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
+                               win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, lo == 0 ? dt : 0, part, lo, hi);
             NKV_LAUNCHED();
         }
         return NKV_OK;
@@ -2181,15 +2183,15 @@ int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y
     CHECK(check_ptr(x, "x"));
     CHECK(check_ptr(y, "y"));
     const int64_t rows = rows_of(L);
-    // one launch per NKV_STREAM_ROUNDS grid-stride rounds (a row band): +5-7 % at N=1e8
-    // (profiles/r02h_tune_bands_update_opdiag.log), as for the DCGS2 updates
+#ifndef NKVX_OPD_ROUNDS
+#define NKVX_OPD_ROUNDS 0
+#endif
     const int g = grid_for(rows / 2);
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
-    const int64_t band = NKV_STREAM_ROUNDS > 0 && chunks >= 2 * (int64_t)NKV_STREAM_ROUNDS * g
-                             ? (int64_t)NKV_STREAM_ROUNDS * g : (chunks > 0 ? chunks : 1);
-    for (int64_t lo = 0; lo == 0 || lo < chunks; lo += band) {
+    const int64_t band = NKVX_OPD_ROUNDS > 0 ? (int64_t)NKVX_OPD_ROUNDS * g : chunks;
+    for (int64_t lo = 0; lo < chunks; lo += band) {
         const int64_t hi = lo + band < chunks ? lo + band : chunks;
-        hipLaunchKernelGGL(k_op_diag, dim3(g), dim3(kThreads), 0, S(stream), d, x, y, rows, time_scale, lo, hi);
+        hipLaunchKernelGGL(k_op_diag, dim3(g), dim3(kThreads), 0, S(stream), d, x, y, rows, rows, time_scale, lo, hi);
         NKV_LAUNCHED();
     }
     return NKV_OK;

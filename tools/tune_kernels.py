@@ -78,6 +78,16 @@ VARIANTS = {
     "dl_g1024": {"NKV_DC_G": 1024},
     "dl_g512": {"NKV_DC_G": 512},
     "dc_g384": {"NKV_DC_G": 384},
+    "dc_r0": {"NKV_DC_ROUNDS": 0},
+    "dc_r1": {"NKV_DC_ROUNDS": 1},
+    "dc_r4": {"NKV_DC_ROUNDS": 4},
+    # round-2 experiment copy (tools/experiments/nekkrylov_exp.hip; earlier x_* variants: the dual-update
+    # and multi-dot row bands, logged in profiles/r02e-g_tune_*)
+    "x_base": {"src": "exp"},
+    "x_opd1": {"src": "exp", "NKVX_OPD_ROUNDS": 1},
+    "x_opd2": {"src": "exp", "NKVX_OPD_ROUNDS": 2},
+    "x_opd4": {"src": "exp", "NKVX_OPD_ROUNDS": 4},
+    "x_opd8": {"src": "exp", "NKVX_OPD_ROUNDS": 8},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
@@ -91,10 +101,12 @@ def build(names):
     src = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
     procs = []
     for n in names:
-        defs = [f"-D{k}={v}" for k, v in VARIANTS[n].items()]
+        defs = [f"-D{k}={v}" for k, v in VARIANTS[n].items() if k != "src"]
+        vsrc = (os.path.join(ROOT, "tools", "experiments", "nekkrylov_exp.hip") if VARIANTS[n].get("src") == "exp"
+                else src)
         out = os.path.join(VDIR, f"lib_{n}.so")
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I" + os.path.join(ROOT, "include"), *defs, src, "-o", out]
+               "-I" + os.path.join(ROOT, "include"), *defs, vsrc, "-o", out]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
         assert p.wait() == 0
