@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, MI355X_MICROARCH.md
-§HBM) of ``bench.py`` into per-launch HBM traffic per kernel family.
+§HBM) of ``bench.py`` into per-launch HBM traffic per kernel family
+(a "launch" = one entry-point call, which may be several back-to-back row-band dispatches).
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7): counters are in KiB;
 FETCH_SIZE reports exactly half of a wide (16 B/lane) coalesced streaming read, so it is doubled
@@ -31,10 +32,31 @@ FAMILIES = {
 }
 
 
+BANDED = ("dcgs2_update", "op_diag")  # families whose entry points issue row-band dispatches
+
+
 def load(d):
+    """Per-CALL counter values per family.  One entry-point call may issue several dispatches back
+    to back (the row bands of the DCGS2 update, NKV_DC_ROUNDS; of the diagonal matvec,
+    NKV_STREAM_ROUNDS): a call = a run of consecutive dispatches of one family in dispatch order
+    (k_reduce_cols, the second reduction stage, does not end a run); its value is their sum."""
+    rows = sorted(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))),
+                  key=lambda r: int(r["Dispatch_Id"]))
     out = collections.defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        out[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    cur_fam, cur = None, None
+    for r in rows:
+        fam = fam_of(r["Kernel_Name"])
+        if fam is not None and fam == cur_fam and fam in BANDED:
+            cur[0] += float(r["Counter_Value"])
+            cur[1] += 1
+            continue
+        if fam is None and "k_reduce_cols" in r["Kernel_Name"]:
+            continue
+        if cur_fam is not None:
+            out[cur_fam].append(tuple(cur))
+        cur_fam, cur = fam, ([float(r["Counter_Value"]), 1] if fam is not None else None)
+    if cur_fam is not None:
+        out[cur_fam].append(tuple(cur))
     return out
 
 
@@ -52,14 +74,15 @@ def main():
     bench = json.load(open(bench_json))
     agg = {}
     for fam in FAMILIES:
-        fv = [v for k, vs in F.items() if fam_of(k) == fam for v in vs]
-        wv = [v for k, vs in W.items() if fam_of(k) == fam for v in vs]
+        fv = [v for v, _ in F.get(fam, [])]
+        wv = [v for v, _ in W.get(fam, [])]
         if not fv:
             continue
         rd = 2.0 * 1024.0 * sum(fv) / len(fv)
         wr = 1024.0 * sum(wv) / len(wv) if wv else 0.0
-        agg[fam] = dict(launches=len(fv), read_bytes_per_launch=rd, write_bytes_per_launch=wr,
-                        hbm_bytes_per_launch=rd + wr)
+        disp = sum(n for _, n in F[fam]) / len(fv)
+        agg[fam] = dict(launches=len(fv), dispatches_per_launch=disp, read_bytes_per_launch=rd,
+                        write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr)
     dom = bench["roofline"]["kernel"]
     rec = dict(kernel_family=dom, E=bench["config"]["E"], m=bench["config"]["m"],
                hbm_bytes_per_launch=agg.get(dom, {}).get("hbm_bytes_per_launch"),
