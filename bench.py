@@ -309,6 +309,11 @@ def main():
         r = os.environ.get("RANK", "0")   # test hooks: a rank that hangs / fails
         time.sleep(float(os.environ.get("NKV_DRY_SLEEP_RANK" + r, "0")))
         sys.exit(int(os.environ.get("NKV_DRY_RC_RANK" + r, "0")))
+    # the contract's ONE JSON line: keep the real stdout for it and send everything else that
+    # writes to fd 1 (gloo's C++ connection banner, library prints) to stderr
+    sys.stdout.flush()
+    args.json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     run(args)
 
 
@@ -567,6 +572,8 @@ def run(args):
                 "avg_launch_ms": round(ph["avg_ms"], 4),
                 "avg_bytes_per_launch": ph["avg_bytes"],
                 "launches": ph["launches"],
+                "scope": "one GPU (the only rank)" if world == 1 else
+                         f"rank 0's shard on its own GPU (1/{world} of N); peak is one GPU's HBM",
             },
             "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                        for k, v in phases.items()},
@@ -574,13 +581,14 @@ def run(args):
             "ritz_rel_err": ritz_err,
             "ritz_top8_rel_err": top_err,
             "ritz_converged": int(conv.sum()),
+            "ritz_top8": [[float(v.real), float(v.imag)] for v in vals[:8]],
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,
             "cpu_optimised": cpu_opt,
             "restart": restart,
             "krylov_schur_leg": ks_leg,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=args.json_out, flush=True)
     comm.barrier()
     import torch.distributed as dist
 
