@@ -4,6 +4,9 @@
 // NKVX_D2_CHUNKS, are logged in profiles/r02e-g_tune_*; the update bands went into the product as
 // NKV_DC_ROUNDS):
 //   NKVX_OPD_ROUNDS=R  the synthetic diagonal matvec as one launch per R grid-stride rounds.
+//   NKVX_D2_ROUNDS=R   the large-problem multi-dot as one launch per R grid-stride rounds of row
+//                      tiles (each block adds its band partials to its own slot: deterministic);
+//                      NKVX_D2_MINJ=J: only from j >= J (one launch below).
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
 // Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
@@ -537,7 +540,9 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
                                                          const double* __restrict__ y,
                                                          const double* __restrict__ w, int64_t sv,
                                                          int tiles_per_field, int n_fields, int x_last,
-                                                         double* __restrict__ partials, int B) {
+                                                         double* __restrict__ partials, int B, int t_lo = 0,
+                                                         int t_hi = -1, int accum = 0) {
+    if (t_hi < 0) t_hi = tiles_per_field;
     // grid (bx, n_wf / n_fields): each block walks n_fields weighted fields per row tile, so with
     // n_fields = n_wf the weights of a tile are read from HBM once instead of once per field.
     // x_last: x IS column j-1 of Q, so that column is not streamed again — its two dots (x.Wx,
@@ -548,7 +553,7 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+    for (int t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
@@ -628,10 +633,11 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
         }
     }
     __syncthreads();
-    const int b = blockIdx.y * gridDim.x + blockIdx.x;
-    for (int c = threadIdx.x; c < 2 * j; c += kThreads)
-        partials[(int64_t)c * B + b] =
-            (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
+    const int b = blockIdx.y * (B / gridDim.y) + blockIdx.x;
+    for (int c = threadIdx.x; c < 2 * j; c += kThreads) {
+        const double v = (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
+        partials[(int64_t)c * B + b] = accum ? partials[(int64_t)c * B + b] + v : v;
+    }
 }
 
 // DCGS2 small dense step (one workgroup).  Columns 0..m-1 of Q are final; column m holds
@@ -1827,9 +1833,21 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     double* part = partials_of(ws);
     if (tpf > 0) {
         const int xl = (flags & NKV_X_IS_LAST) ? 1 : 0;
+#ifndef NKVX_D2_ROUNDS
+#define NKVX_D2_ROUNDS 0
+#endif
+#ifndef NKVX_D2_MINJ
+#define NKVX_D2_MINJ 0
+#endif
+        const int band = (NKVX_D2_ROUNDS > 0 && j >= NKVX_D2_MINJ && tpf >= 2 * NKVX_D2_ROUNDS * bx)
+                             ? NKVX_D2_ROUNDS * bx : tpf;
         if (large)
-            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
-                               Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
+            for (int lo = 0; lo < tpf; lo += band) {
+                const int hi = lo + band < tpf ? lo + band : tpf;
+                const int gb = bx < hi - lo ? bx : hi - lo;
+                hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(gb, gy), dim3(kThreads), 8 * j * sizeof(double),
+                                   st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B, lo, hi, lo > 0 ? 1 : 0);
+            }
         else
             hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double),
                                st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);

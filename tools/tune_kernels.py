@@ -88,6 +88,10 @@ VARIANTS = {
     "x_opd2": {"src": "exp", "NKVX_OPD_ROUNDS": 2},
     "x_opd4": {"src": "exp", "NKVX_OPD_ROUNDS": 4},
     "x_opd8": {"src": "exp", "NKVX_OPD_ROUNDS": 8},
+    "x_d2r1": {"src": "exp", "NKVX_D2_ROUNDS": 1},
+    "x_d2r2": {"src": "exp", "NKVX_D2_ROUNDS": 2},
+    "x_d2r4": {"src": "exp", "NKVX_D2_ROUNDS": 4},
+    "x_d2r8": {"src": "exp", "NKVX_D2_ROUNDS": 8},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
