@@ -203,3 +203,93 @@ def test_ranks_match_one_rank_with_time_in_dot(gpu):
             assert np.max(np.abs(H - H1)) <= 1e-12 * np.max(np.abs(H1)), (mode, rank)
             np.testing.assert_allclose(t, t1, rtol=1e-11, atol=1e-15)   # replicated time, identical on every rank
             assert np.any(np.abs(t) > 1e-3)
+
+
+def _run_ckpt(world_rank_pair, out, port, directory, action, E):
+    """One rank of a sharded checkpoint/restart run (config-1 diagonal operator, k_dim=16):
+    ``write``: the first factorisation with the ifres hook (one KRY file per rank, HES on rank 0);
+    ``resume``: load_restart at mstart=9 and Krylov–Schur to schur_tgt=5; ``full``: uninterrupted."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.checkpoint import ArnoldiCheckpoint, load_restart
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import KrylovSchurConfig
+        from nekstab_next_amd.krylov_schur import krylov_schur
+        from nekstab_next_amd.layout import NekLayout
+        from nekstab_next_amd.operators import DiagOperator
+        from nekstab_next_amd.vector import NekContext
+
+        lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=E).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=32)
+        d, _ = syn.diag_spectrum(lay)
+        op = DiagOperator(ctx, d)
+        cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5)
+        if action == "write":
+            seed = ctx.vector()
+            seed.fill_hash(11)
+            krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=0),
+                         on_step=ArnoldiCheckpoint(ctx, directory, session="cyl", evop="d"))
+        else:
+            if action == "resume":
+                Q, H = load_restart(ctx, directory, "cyl", 9, 16)
+                r = krylov_schur(ctx, op, None, cfg, Q=Q, start=(9, H))
+            else:
+                seed = ctx.vector()
+                seed.fill_hash(11)
+                r = krylov_schur(ctx, op, seed, cfg)
+            out[(action, world, rank)] = (r.vals, r.residual, r.mstart_history, r.schur_cnt)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _spawn(world, *args):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_run_ckpt, args=((r, world), args[0], port, *args[1:])) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+
+
+@pytest.mark.parametrize("w_write,w_resume", [(3, 1), (1, 2)])
+def test_sharded_checkpoint_resumes_at_another_world_size(gpu, tmp_path, w_write, w_resume):
+    """ifres checkpoint written by `w_write` ranks (a Nek5000 multi-file KRY set, one file per rank,
+    HES on rank 0; ragged shards 100/100/101 of E=301) and resumed by `w_resume` ranks, as a
+    Nek5000 restart reads a field-file set written by any number of ranks (the element map places
+    every element; core/IO.f90:12-73 through load_fld).  The resumed run follows the uninterrupted
+    one-rank run: restart count and mstart sequence identical, Ritz values of the comparison set
+    to 1e-10.  The oracle's independent #std reader (oracle/nekio.py) reads the written set into
+    the same Krylov vectors as the one-rank checkpoint's (1e-12 of max |q|)."""
+    import nekio
+
+    E = 301
+    out = mp.Manager().dict()
+    ref_dir, dir_w = str(tmp_path / "one"), str(tmp_path / "w")
+    _spawn(1, out, ref_dir, "write", E)
+    _spawn(1, out, ref_dir, "full", E)
+    _spawn(w_write, out, dir_w, "write", E)
+    _spawn(w_resume, out, dir_w, "resume", E)
+    assert len([f for f in os.listdir(dir_w) if f.startswith("KRYcyl") and f.endswith(".f00005")]) == w_write
+    v1, r1, m1, c1 = out[("full", 1, 0)]
+    conv = r1 < 1e-6
+    sel = sorted(set(np.nonzero(conv)[0].tolist() + list(range(8))))
+    for rank in range(w_resume):
+        v2, r2, m2, c2 = out[("resume", w_resume, rank)]
+        assert m2 == m1 and c2 == c1
+        assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) < 1e-10
+    g = nekio.Geom(2, 6, 4, E)
+    H_ref, Q_ref = nekio.load_restart(ref_dir, "cyl", g, 9, 16, nfiles=1)
+    H_w, Q_w = nekio.load_restart(dir_w, "cyl", g, 9, 16, nfiles=w_write)
+    assert Q_w.shape == Q_ref.shape
+    assert np.max(np.abs(Q_w - Q_ref)) < 1e-12 * np.max(np.abs(Q_ref))
+    assert np.max(np.abs(H_w - H_ref)) < 1e-12 * np.max(np.abs(H_ref))
