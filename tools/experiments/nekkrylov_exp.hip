@@ -1,12 +1,12 @@
 // EXPERIMENT COPY of nekstab_next_amd/csrc/nekkrylov.hip — built only by tools/tune_kernels.py
 // (variants with "src": "exp"), never by build(); the product never loads it.
-// Round-2 experiments (the dual-update row bands, NKVX_CHUNKS/NKVX_ROUNDS and the multi-dot bands
-// NKVX_D2_CHUNKS, are logged in profiles/r02e-g_tune_*; the update bands went into the product as
-// NKV_DC_ROUNDS):
-//   NKVX_OPD_ROUNDS=R  the synthetic diagonal matvec as one launch per R grid-stride rounds.
-//   NKVX_D2_ROUNDS=R   the large-problem multi-dot as one launch per R grid-stride rounds of row
-//                      tiles (each block adds its band partials to its own slot: deterministic);
-//                      NKVX_D2_MINJ=J: only from j >= J (one launch below).
+// Earlier round-2 experiments (row bands of the dual update / multi-dot / matvec) are logged in
+// profiles/r02e-h,m_tune_*; the update and matvec bands went into the product.  This copy:
+//   NKVX_D2_CONTIG=1  the large-problem multi-dot: block b takes the CONTIGUOUS row tiles
+//                     [b T/B, (b+1) T/B) of each field instead of the grid-stride tiles b, b+B, ...
+//                     (consecutive tiles share address-translation pages; profiles/r02q_tlb_by_j.json
+//                     shows the multi-dot's UTCL1 in-flight stalls growing with j)
+//   NKVX_DC_CONTIG=1  the dual update: within a row band, block b takes contiguous tiles.
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
 // Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
@@ -30,6 +30,12 @@
 namespace {
 
 // Tuning knobs (compile-time; tools/tune_kernels.py builds variants and times them on MI355X):
+#ifndef NKVX_D2_CONTIG
+#define NKVX_D2_CONTIG 0
+#endif
+#ifndef NKVX_DC_CONTIG
+#define NKVX_DC_CONTIG 0
+#endif
 #ifndef NKV_PAIRS
 #define NKV_PAIRS 8  // double2 per thread per tile in the dot/update kernels (large problems)
 #endif
@@ -76,6 +82,9 @@ namespace {
 #define NKV_DC_ROUNDS 2  // DCGS2 updates: one launch per this many grid-stride rounds of row tiles (a
                          // "row band"); the launch boundaries keep the grid's loads and stores in one
                          // band: +9-19 % at N=1e8, +0-1 % at the 8-GPU shard (profiles/r02f_tune_*)
+#endif
+#ifndef NKV_STREAM_ROUNDS
+#define NKV_STREAM_ROUNDS 2  // synthetic diagonal matvec: one launch per this many grid-stride rounds
 #endif
 #ifndef NKV_D2_MAXB
 #define NKV_D2_MAXB 256  // workgroups of the two-vector multi-dot: one per CU (+1 % over 1024 at
@@ -540,9 +549,7 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
                                                          const double* __restrict__ y,
                                                          const double* __restrict__ w, int64_t sv,
                                                          int tiles_per_field, int n_fields, int x_last,
-                                                         double* __restrict__ partials, int B, int t_lo = 0,
-                                                         int t_hi = -1, int accum = 0) {
-    if (t_hi < 0) t_hi = tiles_per_field;
+                                                         double* __restrict__ partials, int B) {
     // grid (bx, n_wf / n_fields): each block walks n_fields weighted fields per row tile, so with
     // n_fields = n_wf the weights of a tile are read from HBM once instead of once per field.
     // x_last: x IS column j-1 of Q, so that column is not streamed again — its two dots (x.Wx,
@@ -553,7 +560,13 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-    for (int t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x) {
+#if NKVX_D2_CONTIG
+    const int t_beg = (int)((int64_t)blockIdx.x * tiles_per_field / gridDim.x);
+    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_per_field / gridDim.x);
+    for (int t = t_beg; t < t_end; ++t) {
+#else
+    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+#endif
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
@@ -633,11 +646,10 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
         }
     }
     __syncthreads();
-    const int b = blockIdx.y * (B / gridDim.y) + blockIdx.x;
-    for (int c = threadIdx.x; c < 2 * j; c += kThreads) {
-        const double v = (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
-        partials[(int64_t)c * B + b] = accum ? partials[(int64_t)c * B + b] + v : v;
-    }
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    for (int c = threadIdx.x; c < 2 * j; c += kThreads)
+        partials[(int64_t)c * B + b] =
+            (red[c] + red[2 * j + c]) + (red[4 * j + c] + red[6 * j + c]);
 }
 
 // DCGS2 small dense step (one workgroup).  Columns 0..m-1 of Q are final; column m holds
@@ -925,7 +937,13 @@ void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
     }
     double2 af[kPairs];
     if constexpr (!kNrm) {
+#if NKVX_DC_CONTIG
+        const int nb = t_hi - t_lo;
+        for (int t = t_lo + (int)((int64_t)blockIdx.x * nb / gridDim.x);
+             t < t_lo + (int)((int64_t)(blockIdx.x + 1) * nb / gridDim.x); ++t)
+#else
         for (int t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x)   // this launch's row band
+#endif
             dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af);
         return;
     }
@@ -1393,11 +1411,9 @@ __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q,
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__ d,
                                                       const double* __restrict__ x,
-                                                      double* __restrict__ y, int64_t rows,
-                                                      int64_t time_off, double ts, int64_t c_lo = 0,
-                                                      int64_t c_hi = -1) {
-    const int64_t chunks = c_hi < 0 ? rows / (2 * kThreads * kStreamUnr) : c_hi;
-    for (int64_t ci = c_lo + blockIdx.x; ci < chunks; ci += gridDim.x) {
+                                                      double* __restrict__ y, int64_t time_off, double ts,
+                                                      int64_t c_lo, int64_t c_hi) {
+    for (int64_t ci = c_lo + blockIdx.x; ci < c_hi; ci += gridDim.x) {   // this launch's row band
         const int64_t p0 = ci * kThreads * kStreamUnr + threadIdx.x;
         double2 dv[kStreamUnr], xv[kStreamUnr];
 #pragma unroll
@@ -1409,7 +1425,7 @@ __global__ __launch_bounds__(kThreads) void k_op_diag(const double* __restrict__
         for (int u = 0; u < kStreamUnr; ++u)
             st2p(y, 2 * (p0 + u * kThreads), make_double2(dv[u].x * xv[u].x, dv[u].y * xv[u].y));
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
+    if (c_lo == 0 && blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = ts * x[time_off];
 }
 
 __global__ __launch_bounds__(kThreads) void k_op_rot2(const double* __restrict__ cs,
@@ -1833,21 +1849,9 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     double* part = partials_of(ws);
     if (tpf > 0) {
         const int xl = (flags & NKV_X_IS_LAST) ? 1 : 0;
-#ifndef NKVX_D2_ROUNDS
-#define NKVX_D2_ROUNDS 0
-#endif
-#ifndef NKVX_D2_MINJ
-#define NKVX_D2_MINJ 0
-#endif
-        const int band = (NKVX_D2_ROUNDS > 0 && j >= NKVX_D2_MINJ && tpf >= 2 * NKVX_D2_ROUNDS * bx)
-                             ? NKVX_D2_ROUNDS * bx : tpf;
         if (large)
-            for (int lo = 0; lo < tpf; lo += band) {
-                const int hi = lo + band < tpf ? lo + band : tpf;
-                const int gb = bx < hi - lo ? bx : hi - lo;
-                hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(gb, gy), dim3(kThreads), 8 * j * sizeof(double),
-                                   st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B, lo, hi, lo > 0 ? 1 : 0);
-            }
+            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
+                               Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
         else
             hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double),
                                st, Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
@@ -1909,10 +1913,12 @@ int nkv_dcgs2_update_lazy(const nkv_layout* L, const double* S_cols, int m, cons
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     auto kern = large ? k_dcgs2_lazy_update<NKV_DC_PAIRS> : k_dcgs2_lazy_update<NKV_PAIRS_SMALL>;
     const int band = band_tiles(tiles_total, g);
-    for (int lo = 0; lo < tiles_total; lo += band) {   // one launch per row band (NKV_DC_ROUNDS)
+    // one launch per row band (NKV_DC_ROUNDS); at least one, which also updates the time slot
+    for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {
         const int hi = lo + band < tiles_total ? lo + band : tiles_total;
-        hipLaunchKernelGGL(kern, dim3(g < hi - lo ? g : hi - lo), dim3(kThreads), 0, st, S_cols, L->ld, m, coef_dev,
-                           win, fout, lo, hi, rows_of(L), lo == 0 ? dt : 0);
+        const int gb = g < hi - lo ? g : (hi - lo > 0 ? hi - lo : 1);
+        hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, S_cols, L->ld, m, coef_dev, win, fout, lo, hi,
+                           rows_of(L), lo == 0 ? dt : 0);
         NKV_LAUNCHED();
     }
     return NKV_OK;
@@ -1949,10 +1955,11 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
         // one launch per row band of NKV_DC_ROUNDS grid-stride rounds: every launch boundary is a
         // grid-wide point where all loads and stores of the band have retired (no in-kernel barrier)
         const int band = band_tiles(tiles_total, g);
-        for (int lo = 0; lo < tiles_total; lo += band) {
+        for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {   // >= 1 launch: also the time slot
             const int hi = lo + band < tiles_total ? lo + band : tiles_total;
-            hipLaunchKernelGGL(kern, dim3(g < hi - lo ? g : hi - lo), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj,
-                               win, fout, w, L->sv, tpf, tiles_w, tiles_total, T, lo == 0 ? dt : 0, part, lo, hi);
+            const int gb = g < hi - lo ? g : (hi - lo > 0 ? hi - lo : 1);
+            hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, Q, L->ld, m, coef_dev, qj, win, fout, w, L->sv,
+                               tpf, tiles_w, tiles_total, T, lo == 0 ? dt : 0, part, lo, hi);
             NKV_LAUNCHED();
         }
         return NKV_OK;
@@ -2201,15 +2208,15 @@ int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y
     CHECK(check_ptr(x, "x"));
     CHECK(check_ptr(y, "y"));
     const int64_t rows = rows_of(L);
-#ifndef NKVX_OPD_ROUNDS
-#define NKVX_OPD_ROUNDS 0
-#endif
+    // one launch per NKV_STREAM_ROUNDS grid-stride rounds (a row band): +5-7 % at N=1e8
+    // (profiles/r02h_tune_bands_update_opdiag.log), as for the DCGS2 updates
     const int g = grid_for(rows / 2);
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
-    const int64_t band = NKVX_OPD_ROUNDS > 0 ? (int64_t)NKVX_OPD_ROUNDS * g : chunks;
-    for (int64_t lo = 0; lo < chunks; lo += band) {
+    const int64_t band = NKV_STREAM_ROUNDS > 0 && chunks >= 2 * (int64_t)NKV_STREAM_ROUNDS * g
+                             ? (int64_t)NKV_STREAM_ROUNDS * g : (chunks > 0 ? chunks : 1);
+    for (int64_t lo = 0; lo == 0 || lo < chunks; lo += band) {
         const int64_t hi = lo + band < chunks ? lo + band : chunks;
-        hipLaunchKernelGGL(k_op_diag, dim3(g), dim3(kThreads), 0, S(stream), d, x, y, rows, rows, time_scale, lo, hi);
+        hipLaunchKernelGGL(k_op_diag, dim3(g), dim3(kThreads), 0, S(stream), d, x, y, rows, time_scale, lo, hi);
         NKV_LAUNCHED();
     }
     return NKV_OK;

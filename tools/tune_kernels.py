@@ -84,14 +84,9 @@ VARIANTS = {
     # round-2 experiment copy (tools/experiments/nekkrylov_exp.hip; earlier x_* variants: the dual-update
     # and multi-dot row bands, logged in profiles/r02e-g_tune_*)
     "x_base": {"src": "exp"},
-    "x_opd1": {"src": "exp", "NKVX_OPD_ROUNDS": 1},
-    "x_opd2": {"src": "exp", "NKVX_OPD_ROUNDS": 2},
-    "x_opd4": {"src": "exp", "NKVX_OPD_ROUNDS": 4},
-    "x_opd8": {"src": "exp", "NKVX_OPD_ROUNDS": 8},
-    "x_d2r1": {"src": "exp", "NKVX_D2_ROUNDS": 1},
-    "x_d2r2": {"src": "exp", "NKVX_D2_ROUNDS": 2},
-    "x_d2r4": {"src": "exp", "NKVX_D2_ROUNDS": 4},
-    "x_d2r8": {"src": "exp", "NKVX_D2_ROUNDS": 8},
+    "x_d2c": {"src": "exp", "NKVX_D2_CONTIG": 1},
+    "x_dcc": {"src": "exp", "NKVX_DC_CONTIG": 1},
+    "x_both": {"src": "exp", "NKVX_D2_CONTIG": 1, "NKVX_DC_CONTIG": 1},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
