@@ -1326,12 +1326,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #ifndef NKV_ROTF_U
 #define NKV_ROTF_U 4
 #endif
+#ifndef NKV_ROTF_G
+#define NKV_ROTF_G 768   // workgroups of the few-column rotation
+#endif
+#ifndef NKV_ROTF_ROUNDS
+#define NKV_ROTF_ROUNDS 1   // few-column rotation: one launch per this many grid-stride rounds (0: one launch)
+#endif
 static_assert(NKV_TILE % (kThreads * NKV_ROTF_P * 2) == 0, "rotate-few tile must divide the padding");
 template <int NO, int P, int U>
 __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q, int64_t ld, int k,
-                                                         const double* __restrict__ V, int ldv, int64_t n_tiles) {
+                                                         const double* __restrict__ V, int ldv, int64_t t_lo,
+                                                         int64_t t_hi) {
     constexpr int kTile = kThreads * P * 2;
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    for (int64_t t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x) {   // this launch's row band
         const int64_t r0 = t * kTile + 2 * threadIdx.x;
         const double* qb = Q + r0;
         double2 acc[NO][P];
@@ -2115,10 +2122,16 @@ static int launch_rotate_few(const nkv_layout* L, double* Q, int k, const double
     constexpr int P = NKV_ROTF_P, U = NKV_ROTF_U;
     const int64_t n_tiles = rows_of(L) / (kThreads * P * 2);
     if (n_tiles < 1) return NKV_OK;
-    const int64_t g = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
-    hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)g), dim3(kThreads), 0, S(stream), Q, L->ld, k, V,
-                       ldv, n_tiles);
-    NKV_LAUNCHED();
+    // one launch per row band of NKV_ROTF_ROUNDS grid-stride rounds of an NKV_ROTF_G grid, as the DCGS2
+    // updates: +17-21 % at N=1e8 over one 1024-workgroup launch (profiles/r02s_tune_rotf*.log)
+    const int64_t g = n_tiles < NKV_ROTF_G ? n_tiles : NKV_ROTF_G;
+    const int64_t band = NKV_ROTF_ROUNDS > 0 ? (int64_t)NKV_ROTF_ROUNDS * g : n_tiles;
+    for (int64_t lo = 0; lo < n_tiles; lo += band) {
+        const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
+        hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(kThreads), 0,
+                           S(stream), Q, L->ld, k, V, ldv, lo, hi);
+        NKV_LAUNCHED();
+    }
     return NKV_OK;
 }
 

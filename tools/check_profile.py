@@ -71,6 +71,24 @@ def main():
         kept_key = f"k_rotate_few<{n_kept}," if n_kept <= 8 else f"k_rotate_stream<1, {(n_kept + 15) // 16},"
         for label, key, ms in (("rotate kept", kept_key, rs["rotate_kept_ms"]),
                                ("rotate full", "k_rotate_stream<1, 8,", rs["rotate_full_ms"])):
+            if trace and key.startswith("k_rotate_few"):
+                # one call = a run of consecutive dispatches (the few-column rotation issues one per
+                # row band, NKV_ROTF_ROUNDS); its duration spans first start .. last end
+                spans, cur = [], None
+                for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
+                    if key in r["Kernel_Name"]:
+                        s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                        cur = [s0, e0, 1] if cur is None else [cur[0], e0, cur[2] + 1]
+                    elif cur is not None:
+                        spans.append(cur)
+                        cur = None
+                if cur is not None:
+                    spans.append(cur)
+                if spans:
+                    avg = sum((e - s0) for s0, e, _ in spans) / len(spans) / 1e6
+                    print(f"{label:14s} {len(spans):13d} {avg:15.4f} {'':>16s} {ms:14.4f} {ms / avg:7.3f}"
+                          f"  ({spans[0][2]} disp/call)")
+                    continue
             rows = [r for r in stats if key in r["Name"]]
             if rows:
                 calls = sum(int(r["Calls"]) for r in rows)

@@ -7,6 +7,9 @@
 //                     (consecutive tiles share address-translation pages; profiles/r02q_tlb_by_j.json
 //                     shows the multi-dot's UTCL1 in-flight stalls growing with j)
 //   NKVX_DC_CONTIG=1  the dual update: within a row band, block b takes contiguous tiles.
+//   NKVX_ROTF_ROUNDS=R / NKVX_ROTF_G=G  the few-column restart rotation as one launch per R
+//                     grid-stride rounds of a G-workgroup grid (row bands, as the dual update).
+//   NKVX_ROTS_ROUNDS=R  the MFMA streaming rotation (n_out > 8) as one launch per R grid-stride rounds.
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
 // Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
@@ -1281,7 +1284,7 @@ __global__ __launch_bounds__(kThreads) void k_rotate_mfma(double* __restrict__ Q
 template <int NB, int MB, int WAVES, int U>
 __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict__ Q, int64_t ld, int k,
                                                               const double* __restrict__ V, int ldv, int n_out,
-                                                              int kp, int64_t n_tiles) {
+                                                              int kp, int64_t n_tiles, int64_t t_lo = 0) {
     extern __shared__ __attribute__((aligned(16))) double Vs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
@@ -1292,7 +1295,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     }
     __syncthreads();
     const double* vs = Vs + lr * kp + lk;
-    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    for (int64_t tile = t_lo + blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t row0 = (tile * WAVES + wave) * (NB * 16);
         const double* q = Q + row0 + lr;
         nkv_f64x4 acc[NB][MB];
@@ -1356,9 +1359,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 static_assert(NKV_TILE % (kThreads * NKV_ROTF_P * 2) == 0, "rotate-few tile must divide the padding");
 template <int NO, int P, int U>
 __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q, int64_t ld, int k,
-                                                         const double* __restrict__ V, int ldv, int64_t n_tiles) {
+                                                         const double* __restrict__ V, int ldv, int64_t n_tiles,
+                                                         int64_t t_lo = 0) {
     constexpr int kTile = kThreads * P * 2;
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    for (int64_t t = t_lo + blockIdx.x; t < n_tiles; t += gridDim.x) {
         const int64_t r0 = t * kTile + 2 * threadIdx.x;
         const double* qb = Q + r0;
         double2 acc[NO][P];
@@ -2131,8 +2135,15 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
     per_cu = per_cu < 1 ? 1 : (per_cu > 32 / W ? 32 / W : per_cu);   // LDS and 32 waves per CU
     const int64_t g0 = (int64_t)device_cus() * per_cu;
     const int64_t g = n_tiles < g0 ? n_tiles : g0;
-    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, kp,
-                       n_tiles);
+#ifndef NKVX_ROTS_ROUNDS
+#define NKVX_ROTS_ROUNDS 0
+#endif
+    const int64_t band = (NKVX_ROTS_ROUNDS > 0 && n_tiles >= 2 * NKVX_ROTS_ROUNDS * g) ? NKVX_ROTS_ROUNDS * g : n_tiles;
+    for (int64_t lo = 0; lo < n_tiles; lo += band) {
+        const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(W * 64), lds, S(stream), Q, L->ld,
+                           k, V, ldv, n_out, kp, hi, lo);
+    }
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -2142,9 +2153,19 @@ static int launch_rotate_few(const nkv_layout* L, double* Q, int k, const double
     constexpr int P = NKV_ROTF_P, U = NKV_ROTF_U;
     const int64_t n_tiles = rows_of(L) / (kThreads * P * 2);
     if (n_tiles < 1) return NKV_OK;
-    const int64_t g = n_tiles < kMaxBlocks ? n_tiles : kMaxBlocks;
-    hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)g), dim3(kThreads), 0, S(stream), Q, L->ld, k, V,
-                       ldv, n_tiles);
+#ifndef NKVX_ROTF_G
+#define NKVX_ROTF_G kMaxBlocks
+#endif
+#ifndef NKVX_ROTF_ROUNDS
+#define NKVX_ROTF_ROUNDS 0
+#endif
+    const int64_t g = n_tiles < NKVX_ROTF_G ? n_tiles : NKVX_ROTF_G;
+    const int64_t band = (NKVX_ROTF_ROUNDS > 0 && n_tiles >= 2 * NKVX_ROTF_ROUNDS * g) ? NKVX_ROTF_ROUNDS * g : n_tiles;
+    for (int64_t lo = 0; lo < n_tiles; lo += band) {
+        const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
+        hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(kThreads), 0,
+                           S(stream), Q, L->ld, k, V, ldv, hi, lo);
+    }
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -32,14 +32,15 @@ FAMILIES = {
 }
 
 
-BANDED = ("dcgs2_update", "op_diag")  # families whose entry points issue row-band dispatches
+BANDED = ("dcgs2_update", "op_diag", "rotate_kept")  # families whose entry points issue row-band dispatches
 
 
 def load(d):
     """Per-CALL counter values per family.  One entry-point call may issue several dispatches back
     to back (the row bands of the DCGS2 update, NKV_DC_ROUNDS; of the diagonal matvec,
-    NKV_STREAM_ROUNDS): a call = a run of consecutive dispatches of one family in dispatch order
-    (k_reduce_cols, the second reduction stage, does not end a run); its value is their sum."""
+    NKV_STREAM_ROUNDS; of the few-column restart rotation, NKV_ROTF_ROUNDS): a call = a run of
+    consecutive dispatches of one family in dispatch order (k_reduce_cols, the second reduction
+    stage, does not end a run); its value is their sum."""
     rows = sorted(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))),
                   key=lambda r: int(r["Dispatch_Id"]))
     out = collections.defaultdict(list)

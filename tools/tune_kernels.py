@@ -87,6 +87,25 @@ VARIANTS = {
     "x_d2c": {"src": "exp", "NKVX_D2_CONTIG": 1},
     "x_dcc": {"src": "exp", "NKVX_DC_CONTIG": 1},
     "x_both": {"src": "exp", "NKVX_D2_CONTIG": 1, "NKVX_DC_CONTIG": 1},
+    "x_rf_r2": {"src": "exp", "NKVX_ROTF_ROUNDS": 2},
+    "x_rf_r2_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 768},
+    "x_rf_r2_p8u2": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKV_ROTF_P": 8, "NKV_ROTF_U": 2},
+    "x_rf_r2_p8u2_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKV_ROTF_P": 8, "NKV_ROTF_U": 2, "NKVX_ROTF_G": 768},
+    "x_rf_p8u2": {"src": "exp", "NKV_ROTF_P": 8, "NKV_ROTF_U": 2},
+    "x_rf_r4": {"src": "exp", "NKVX_ROTF_ROUNDS": 4},
+    "x_rf_r1_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 768},
+    "x_rf_r3_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 3, "NKVX_ROTF_G": 768},
+    "x_rf_r2_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 512},
+    "x_rf_r2_g256": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 256},
+    "x_rf_r4_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 4, "NKVX_ROTF_G": 512},
+    "x_rf_r2_g768_p2u8": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 768, "NKV_ROTF_P": 2, "NKV_ROTF_U": 8},
+    "x_rf_r1_g1024": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 1024},
+    "x_rf_r1_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 512},
+    "x_rf_r1_g640": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 640},
+    "x_rf_r1_g896": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 896},
+    "x_rs_r4": {"src": "exp", "NKVX_ROTS_ROUNDS": 4},
+    "x_rs_r16": {"src": "exp", "NKVX_ROTS_ROUNDS": 16},
+    "x_rs_r64": {"src": "exp", "NKVX_ROTS_ROUNDS": 64},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
