@@ -9,6 +9,7 @@
 //   NKVX_DC_CONTIG=1  the dual update: within a row band, block b takes contiguous tiles.
 //   NKVX_ROTF_ROUNDS=R / NKVX_ROTF_G=G  the few-column restart rotation as one launch per R
 //                     grid-stride rounds of a G-workgroup grid (row bands, as the dual update).
+//   NKVX_OPD_G=G      workgroups of the synthetic diagonal matvec (with NKV_STREAM_ROUNDS rounds per band).
 //   NKVX_ROTS_ROUNDS=R  the MFMA streaming rotation (n_out > 8) as one launch per R grid-stride rounds.
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
@@ -2231,7 +2232,10 @@ int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y
     const int64_t rows = rows_of(L);
     // one launch per NKV_STREAM_ROUNDS grid-stride rounds (a row band): +5-7 % at N=1e8
     // (profiles/r02h_tune_bands_update_opdiag.log), as for the DCGS2 updates
-    const int g = grid_for(rows / 2);
+#ifndef NKVX_OPD_G
+#define NKVX_OPD_G NKV_STREAM_G
+#endif
+    const int g = grid_for(rows / 2, NKVX_OPD_G);
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
     const int64_t band = NKV_STREAM_ROUNDS > 0 && chunks >= 2 * (int64_t)NKV_STREAM_ROUNDS * g
                              ? (int64_t)NKV_STREAM_ROUNDS * g : (chunks > 0 ? chunks : 1);

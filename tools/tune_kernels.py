@@ -106,6 +106,15 @@ VARIANTS = {
     "x_rs_r4": {"src": "exp", "NKVX_ROTS_ROUNDS": 4},
     "x_rs_r16": {"src": "exp", "NKVX_ROTS_ROUNDS": 16},
     "x_rs_r64": {"src": "exp", "NKVX_ROTS_ROUNDS": 64},
+    "x_opd_g768_r1": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 1},
+    "x_opd_g768_r2": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 2},
+    "x_opd_g768_r4": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 4},
+    "x_opd_g1024_r1": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 1},
+    "x_opd_g1024_r2": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 2},
+    "x_opd_g1024_r4": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 4},
+    "x_opd_g2048_r1": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 1},
+    "x_opd_g2048_r2": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 2},
+    "x_opd_g2048_r4": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 4},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
