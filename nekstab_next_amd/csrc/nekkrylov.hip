@@ -1318,7 +1318,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 // outputs are stored and no other thread touches that row, so in place is safe.
 // ------------------------------------------------------------------------------------------
 #ifndef NKV_ROTF_MAX
-#define NKV_ROTF_MAX 8   // 0: never use the few-column rotation
+#define NKV_ROTF_MAX 16   // 0: never use the few-column rotation
 #endif
 #ifndef NKV_ROTF_P
 #define NKV_ROTF_P 4
@@ -1333,6 +1333,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #define NKV_ROTF_ROUNDS 1   // few-column rotation: one launch per this many grid-stride rounds (0: one launch)
 #endif
 static_assert(NKV_TILE % (kThreads * NKV_ROTF_P * 2) == 0, "rotate-few tile must divide the padding");
+static_assert(NKV_TILE % (kThreads * 2 * 2) == 0, "rotate-few tile (9-16 kept columns) must divide the padding");
 template <int NO, int P, int U>
 __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q, int64_t ld, int k,
                                                          const double* __restrict__ V, int ldv, int64_t t_lo,
@@ -2119,7 +2120,10 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
 
 extern "C++" template <int NO>
 static int launch_rotate_few(const nkv_layout* L, double* Q, int k, const double* V, int ldv, void* stream) {
-    constexpr int P = NKV_ROTF_P, U = NKV_ROTF_U;
+    // NO accumulators per row pair: past 8 kept columns fewer row pairs per thread keep the register
+    // budget (9-12: 2 pairs x 2 columns in flight, 130 VGPRs at NO = 12; 13-16: 2 x 4) — +32 % at
+    // NO = 12 and +10 % at NO = 16 over the MFMA streaming rotation (profiles/r02v_tune_rotf16_E44176.log)
+    constexpr int P = NO <= 8 ? NKV_ROTF_P : 2, U = NO <= 8 ? NKV_ROTF_U : (NO <= 12 ? 2 : 4);
     const int64_t n_tiles = rows_of(L) / (kThreads * P * 2);
     if (n_tiles < 1) return NKV_OK;
     // one launch per row band of NKV_ROTF_ROUNDS grid-stride rounds of an NKV_ROTF_G grid, as the DCGS2
@@ -2155,6 +2159,14 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
             case 6: return launch_rotate_few<6>(L, Q, k, V_dev, ldv, stream);
             case 7: return launch_rotate_few<7>(L, Q, k, V_dev, ldv, stream);
             case 8: return launch_rotate_few<8>(L, Q, k, V_dev, ldv, stream);
+            case 9: return launch_rotate_few<9>(L, Q, k, V_dev, ldv, stream);
+            case 10: return launch_rotate_few<10>(L, Q, k, V_dev, ldv, stream);
+            case 11: return launch_rotate_few<11>(L, Q, k, V_dev, ldv, stream);
+            case 12: return launch_rotate_few<12>(L, Q, k, V_dev, ldv, stream);
+            case 13: return launch_rotate_few<13>(L, Q, k, V_dev, ldv, stream);
+            case 14: return launch_rotate_few<14>(L, Q, k, V_dev, ldv, stream);
+            case 15: return launch_rotate_few<15>(L, Q, k, V_dev, ldv, stream);
+            case 16: return launch_rotate_few<16>(L, Q, k, V_dev, ldv, stream);
             default: break;
         }
     }

@@ -206,7 +206,8 @@ def test_rotate_vs_oracle(gpu, k):
 
 
 @pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 6), (128, 8), (9, 9), (4, 4), (131, 5), (576, 7),
-                                     (128, 20), (129, 17), (256, 255), (300, 150), (576, 33), (900, 6)])
+                                     (128, 12), (130, 13), (64, 16), (1000, 11), (128, 20), (129, 17), (256, 255),
+                                     (300, 150), (576, 33), (900, 6)])
 def test_rotate_cols_vs_oracle(gpu, k, n_out):
     """Partial restart rotation: Q[:, :n_out] = Q[:, :k] V[:, :n_out]; columns n_out..k untouched."""
     lay = LAYOUTS["2d"]
@@ -232,6 +233,32 @@ def test_rotate_cols_vs_oracle(gpu, k, n_out):
         np.testing.assert_allclose(syn.to_reference_order(lay, got[i]), Qk[i], rtol=1e-12, atol=1e-13)
     for i in range(n_out, k + 1):
         np.testing.assert_array_equal(syn.to_reference_order(lay, got[i]), Qref[i])
+
+
+@pytest.mark.parametrize("n_out", [6, 12, 16, 17])
+def test_rotate_cols_row_bands(gpu, n_out):
+    """The few-column rotation issues one dispatch per row band (NKV_ROTF_ROUNDS): at N=2.26e6
+    (E=1000, 3-D) a call spans several bands; every band's rows equal Q V to 1e-12 and the
+    columns past n_out are untouched (n_out=17 runs the MFMA streaming kernel beside it)."""
+    from nekstab_next_amd.layout import box3d_layout
+
+    lay = box3d_layout(1000)
+    ctx, _ = make_ctx(lay)
+    k = 20
+    Q = ctx.basis(k + 1)
+    for i in range(k + 1):
+        Q[i].fill_hash(300 + i)
+    before = Q.storage.cpu().numpy().copy()
+    V = np.linalg.qr(np.random.default_rng(n_out).standard_normal((k, k)))[0][:, :n_out]
+    Vd = torch.as_tensor(np.asfortranarray(V).ravel(order="F")).to(ctx.device)
+    ctx.call("nkv_rotate_cols", Q.ptr, k, Vd.data_ptr(), k, n_out, ctx.stream)
+    got = Q.storage.cpu().numpy()
+    rows = lay.rows   # streamed rows; the time slot and the padding after it are not rotated
+    want = V.T @ before[:k, :rows]
+    for i in range(n_out):
+        np.testing.assert_allclose(got[i, :rows], want[i], rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(got[:n_out, rows:], before[:n_out, rows:])
+    np.testing.assert_array_equal(got[n_out:], before[n_out:])
 
 
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2", "dcgs2-lazy"])

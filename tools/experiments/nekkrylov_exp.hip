@@ -1,16 +1,11 @@
 // EXPERIMENT COPY of nekstab_next_amd/csrc/nekkrylov.hip — built only by tools/tune_kernels.py
 // (variants with "src": "exp"), never by build(); the product never loads it.
-// Earlier round-2 experiments (row bands of the dual update / multi-dot / matvec) are logged in
-// profiles/r02e-h,m_tune_*; the update and matvec bands went into the product.  This copy:
-//   NKVX_D2_CONTIG=1  the large-problem multi-dot: block b takes the CONTIGUOUS row tiles
-//                     [b T/B, (b+1) T/B) of each field instead of the grid-stride tiles b, b+B, ...
-//                     (consecutive tiles share address-translation pages; profiles/r02q_tlb_by_j.json
-//                     shows the multi-dot's UTCL1 in-flight stalls growing with j)
-//   NKVX_DC_CONTIG=1  the dual update: within a row band, block b takes contiguous tiles.
-//   NKVX_ROTF_ROUNDS=R / NKVX_ROTF_G=G  the few-column restart rotation as one launch per R
-//                     grid-stride rounds of a G-workgroup grid (row bands, as the dual update).
-//   NKVX_OPD_G=G      workgroups of the synthetic diagonal matvec (with NKV_STREAM_ROUNDS rounds per band).
-//   NKVX_ROTS_ROUNDS=R  the MFMA streaming rotation (n_out > 8) as one launch per R grid-stride rounds.
+// Earlier round-2 experiments (row bands of the dual update / multi-dot / matvec / restart
+// rotations, contiguous tile ranges, matvec grids) are logged in profiles/r02e-h,m,r,s,u_tune_*;
+// the update, matvec and few-column-rotation bands went into the product.  This copy:
+//   NKVX_ROTF16=1     the few-column restart rotation also for 9..16 kept columns (the product sends
+//                     those to the MFMA streaming kernel), with NKVX_ROTF_P16 row pairs per thread
+//                     and NKVX_ROTF_U16 columns in flight.
 // nekkrylov.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for nekStab's Krylov hot path.
 //
 // Layout, flags and the reference functions each entry point replaces: include/nekkrylov.h.
@@ -34,12 +29,6 @@
 namespace {
 
 // Tuning knobs (compile-time; tools/tune_kernels.py builds variants and times them on MI355X):
-#ifndef NKVX_D2_CONTIG
-#define NKVX_D2_CONTIG 0
-#endif
-#ifndef NKVX_DC_CONTIG
-#define NKVX_DC_CONTIG 0
-#endif
 #ifndef NKV_PAIRS
 #define NKV_PAIRS 8  // double2 per thread per tile in the dot/update kernels (large problems)
 #endif
@@ -564,13 +553,7 @@ void k_block_dot2(const double* __restrict__ Q, int64_t ld,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int c = threadIdx.x; c < 8 * j; c += kThreads) red[c] = 0.0;
     __syncthreads();
-#if NKVX_D2_CONTIG
-    const int t_beg = (int)((int64_t)blockIdx.x * tiles_per_field / gridDim.x);
-    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_per_field / gridDim.x);
-    for (int t = t_beg; t < t_end; ++t) {
-#else
     for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
-#endif
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wv[kPairs];
 #pragma unroll
@@ -941,13 +924,7 @@ void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
     }
     double2 af[kPairs];
     if constexpr (!kNrm) {
-#if NKVX_DC_CONTIG
-        const int nb = t_hi - t_lo;
-        for (int t = t_lo + (int)((int64_t)blockIdx.x * nb / gridDim.x);
-             t < t_lo + (int)((int64_t)(blockIdx.x + 1) * nb / gridDim.x); ++t)
-#else
         for (int t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x)   // this launch's row band
-#endif
             dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, (int64_t)t * kTile + 2 * threadIdx.x, af);
         return;
     }
@@ -1285,7 +1262,7 @@ __global__ __launch_bounds__(kThreads) void k_rotate_mfma(double* __restrict__ Q
 template <int NB, int MB, int WAVES, int U>
 __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict__ Q, int64_t ld, int k,
                                                               const double* __restrict__ V, int ldv, int n_out,
-                                                              int kp, int64_t n_tiles, int64_t t_lo = 0) {
+                                                              int kp, int64_t n_tiles) {
     extern __shared__ __attribute__((aligned(16))) double Vs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
@@ -1296,7 +1273,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     }
     __syncthreads();
     const double* vs = Vs + lr * kp + lk;
-    for (int64_t tile = t_lo + blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t row0 = (tile * WAVES + wave) * (NB * 16);
         const double* q = Q + row0 + lr;
         nkv_f64x4 acc[NB][MB];
@@ -1357,13 +1334,20 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #ifndef NKV_ROTF_U
 #define NKV_ROTF_U 4
 #endif
+#ifndef NKV_ROTF_G
+#define NKV_ROTF_G 768   // workgroups of the few-column rotation
+#endif
+#ifndef NKV_ROTF_ROUNDS
+#define NKV_ROTF_ROUNDS 1   // few-column rotation: one launch per this many grid-stride rounds (0: one launch)
+#endif
 static_assert(NKV_TILE % (kThreads * NKV_ROTF_P * 2) == 0, "rotate-few tile must divide the padding");
+static_assert(NKV_TILE % (kThreads * 8 * 2) == 0, "rotate-few tile must divide the padding");
 template <int NO, int P, int U>
 __global__ __launch_bounds__(kThreads) void k_rotate_few(double* __restrict__ Q, int64_t ld, int k,
-                                                         const double* __restrict__ V, int ldv, int64_t n_tiles,
-                                                         int64_t t_lo = 0) {
+                                                         const double* __restrict__ V, int ldv, int64_t t_lo,
+                                                         int64_t t_hi) {
     constexpr int kTile = kThreads * P * 2;
-    for (int64_t t = t_lo + blockIdx.x; t < n_tiles; t += gridDim.x) {
+    for (int64_t t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x) {   // this launch's row band
         const int64_t r0 = t * kTile + 2 * threadIdx.x;
         const double* qb = Q + r0;
         double2 acc[NO][P];
@@ -2136,38 +2120,36 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
     per_cu = per_cu < 1 ? 1 : (per_cu > 32 / W ? 32 / W : per_cu);   // LDS and 32 waves per CU
     const int64_t g0 = (int64_t)device_cus() * per_cu;
     const int64_t g = n_tiles < g0 ? n_tiles : g0;
-#ifndef NKVX_ROTS_ROUNDS
-#define NKVX_ROTS_ROUNDS 0
-#endif
-    const int64_t band = (NKVX_ROTS_ROUNDS > 0 && n_tiles >= 2 * NKVX_ROTS_ROUNDS * g) ? NKVX_ROTS_ROUNDS * g : n_tiles;
-    for (int64_t lo = 0; lo < n_tiles; lo += band) {
-        const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
-        hipLaunchKernelGGL(kern, dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(W * 64), lds, S(stream), Q, L->ld,
-                           k, V, ldv, n_out, kp, hi, lo);
-    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, kp,
+                       n_tiles);
     NKV_LAUNCHED();
     return NKV_OK;
 }
 
+#ifndef NKVX_ROTF16
+#define NKVX_ROTF16 0
+#endif
+#ifndef NKVX_ROTF_P16
+#define NKVX_ROTF_P16 2
+#endif
+#ifndef NKVX_ROTF_U16
+#define NKVX_ROTF_U16 4
+#endif
 extern "C++" template <int NO>
 static int launch_rotate_few(const nkv_layout* L, double* Q, int k, const double* V, int ldv, void* stream) {
-    constexpr int P = NKV_ROTF_P, U = NKV_ROTF_U;
+    constexpr int P = NO <= 8 ? NKV_ROTF_P : NKVX_ROTF_P16, U = NO <= 8 ? NKV_ROTF_U : NKVX_ROTF_U16;
     const int64_t n_tiles = rows_of(L) / (kThreads * P * 2);
     if (n_tiles < 1) return NKV_OK;
-#ifndef NKVX_ROTF_G
-#define NKVX_ROTF_G kMaxBlocks
-#endif
-#ifndef NKVX_ROTF_ROUNDS
-#define NKVX_ROTF_ROUNDS 0
-#endif
-    const int64_t g = n_tiles < NKVX_ROTF_G ? n_tiles : NKVX_ROTF_G;
-    const int64_t band = (NKVX_ROTF_ROUNDS > 0 && n_tiles >= 2 * NKVX_ROTF_ROUNDS * g) ? NKVX_ROTF_ROUNDS * g : n_tiles;
+    // one launch per row band of NKV_ROTF_ROUNDS grid-stride rounds of an NKV_ROTF_G grid, as the DCGS2
+    // updates: +17-21 % at N=1e8 over one 1024-workgroup launch (profiles/r02s_tune_rotf*.log)
+    const int64_t g = n_tiles < NKV_ROTF_G ? n_tiles : NKV_ROTF_G;
+    const int64_t band = NKV_ROTF_ROUNDS > 0 ? (int64_t)NKV_ROTF_ROUNDS * g : n_tiles;
     for (int64_t lo = 0; lo < n_tiles; lo += band) {
         const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
         hipLaunchKernelGGL((k_rotate_few<NO, P, U>), dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(kThreads), 0,
-                           S(stream), Q, L->ld, k, V, ldv, hi, lo);
+                           S(stream), Q, L->ld, k, V, ldv, lo, hi);
+        NKV_LAUNCHED();
     }
-    NKV_LAUNCHED();
     return NKV_OK;
 }
 
@@ -2191,6 +2173,19 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
             case 6: return launch_rotate_few<6>(L, Q, k, V_dev, ldv, stream);
             case 7: return launch_rotate_few<7>(L, Q, k, V_dev, ldv, stream);
             case 8: return launch_rotate_few<8>(L, Q, k, V_dev, ldv, stream);
+            default: break;
+        }
+    }
+    if (NKVX_ROTF16 && n_out <= 16) {
+        switch (n_out) {
+            case 9: return launch_rotate_few<9>(L, Q, k, V_dev, ldv, stream);
+            case 10: return launch_rotate_few<10>(L, Q, k, V_dev, ldv, stream);
+            case 11: return launch_rotate_few<11>(L, Q, k, V_dev, ldv, stream);
+            case 12: return launch_rotate_few<12>(L, Q, k, V_dev, ldv, stream);
+            case 13: return launch_rotate_few<13>(L, Q, k, V_dev, ldv, stream);
+            case 14: return launch_rotate_few<14>(L, Q, k, V_dev, ldv, stream);
+            case 15: return launch_rotate_few<15>(L, Q, k, V_dev, ldv, stream);
+            case 16: return launch_rotate_few<16>(L, Q, k, V_dev, ldv, stream);
             default: break;
         }
     }
@@ -2232,10 +2227,7 @@ int nkv_op_diag(const nkv_layout* L, const double* d, const double* x, double* y
     const int64_t rows = rows_of(L);
     // one launch per NKV_STREAM_ROUNDS grid-stride rounds (a row band): +5-7 % at N=1e8
     // (profiles/r02h_tune_bands_update_opdiag.log), as for the DCGS2 updates
-#ifndef NKVX_OPD_G
-#define NKVX_OPD_G NKV_STREAM_G
-#endif
-    const int g = grid_for(rows / 2, NKVX_OPD_G);
+    const int g = grid_for(rows / 2);
     const int64_t chunks = rows / (2 * kThreads * kStreamUnr);
     const int64_t band = NKV_STREAM_ROUNDS > 0 && chunks >= 2 * (int64_t)NKV_STREAM_ROUNDS * g
                              ? (int64_t)NKV_STREAM_ROUNDS * g : (chunks > 0 ? chunks : 1);

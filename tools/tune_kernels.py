@@ -84,37 +84,10 @@ VARIANTS = {
     # round-2 experiment copy (tools/experiments/nekkrylov_exp.hip; earlier x_* variants: the dual-update
     # and multi-dot row bands, logged in profiles/r02e-g_tune_*)
     "x_base": {"src": "exp"},
-    "x_d2c": {"src": "exp", "NKVX_D2_CONTIG": 1},
-    "x_dcc": {"src": "exp", "NKVX_DC_CONTIG": 1},
-    "x_both": {"src": "exp", "NKVX_D2_CONTIG": 1, "NKVX_DC_CONTIG": 1},
-    "x_rf_r2": {"src": "exp", "NKVX_ROTF_ROUNDS": 2},
-    "x_rf_r2_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 768},
-    "x_rf_r2_p8u2": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKV_ROTF_P": 8, "NKV_ROTF_U": 2},
-    "x_rf_r2_p8u2_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKV_ROTF_P": 8, "NKV_ROTF_U": 2, "NKVX_ROTF_G": 768},
-    "x_rf_p8u2": {"src": "exp", "NKV_ROTF_P": 8, "NKV_ROTF_U": 2},
-    "x_rf_r4": {"src": "exp", "NKVX_ROTF_ROUNDS": 4},
-    "x_rf_r1_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 768},
-    "x_rf_r3_g768": {"src": "exp", "NKVX_ROTF_ROUNDS": 3, "NKVX_ROTF_G": 768},
-    "x_rf_r2_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 512},
-    "x_rf_r2_g256": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 256},
-    "x_rf_r4_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 4, "NKVX_ROTF_G": 512},
-    "x_rf_r2_g768_p2u8": {"src": "exp", "NKVX_ROTF_ROUNDS": 2, "NKVX_ROTF_G": 768, "NKV_ROTF_P": 2, "NKV_ROTF_U": 8},
-    "x_rf_r1_g1024": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 1024},
-    "x_rf_r1_g512": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 512},
-    "x_rf_r1_g640": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 640},
-    "x_rf_r1_g896": {"src": "exp", "NKVX_ROTF_ROUNDS": 1, "NKVX_ROTF_G": 896},
-    "x_rs_r4": {"src": "exp", "NKVX_ROTS_ROUNDS": 4},
-    "x_rs_r16": {"src": "exp", "NKVX_ROTS_ROUNDS": 16},
-    "x_rs_r64": {"src": "exp", "NKVX_ROTS_ROUNDS": 64},
-    "x_opd_g768_r1": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 1},
-    "x_opd_g768_r2": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 2},
-    "x_opd_g768_r4": {"src": "exp", "NKVX_OPD_G": 768, "NKV_STREAM_ROUNDS": 4},
-    "x_opd_g1024_r1": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 1},
-    "x_opd_g1024_r2": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 2},
-    "x_opd_g1024_r4": {"src": "exp", "NKVX_OPD_G": 1024, "NKV_STREAM_ROUNDS": 4},
-    "x_opd_g2048_r1": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 1},
-    "x_opd_g2048_r2": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 2},
-    "x_opd_g2048_r4": {"src": "exp", "NKVX_OPD_G": 2048, "NKV_STREAM_ROUNDS": 4},
+    "x_rf16_p2u4": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 2, "NKVX_ROTF_U16": 4},
+    "x_rf16_p2u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 2, "NKVX_ROTF_U16": 2},
+    "x_rf16_p1u8": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 1, "NKVX_ROTF_U16": 8},
+    "x_rf16_p4u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 4, "NKVX_ROTF_U16": 2},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
@@ -223,6 +196,10 @@ def run(names, E, rounds, js, only=None):
             "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
             "rotate": (lambda: L.nkv_rotate(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, st), 16.0 * j * N),
             "rotate_6": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, 6, st), 8.0 * (j + 6) * N),
+            "rotate_12": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(12, j), st),
+                          8.0 * (j + min(12, j)) * N),
+            "rotate_16": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(16, j), st),
+                          8.0 * (j + min(16, j)) * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
         }
