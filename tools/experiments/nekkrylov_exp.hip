@@ -3,6 +3,9 @@
 // Earlier round-2 experiments (row bands of the dual update / multi-dot / matvec / restart
 // rotations, contiguous tile ranges, matvec grids) are logged in profiles/r02e-h,m,r,s,u_tune_*;
 // the update, matvec and few-column-rotation bands went into the product.  This copy:
+//   NKVX_BD_ROUNDS=R  the single-vector multi-dot (CGS2 passes, closing re-orthogonalisation) as one
+//                     launch per R grid-stride rounds (band partials accumulated per block).
+//   NKVX_BU_ROUNDS=R / NKVX_BU_G=G  the block update (f -= Q h, optional norm partial) likewise.
 //   NKVX_ROTF16=1     the few-column restart rotation also for 9..16 kept columns (the product sends
 //                     those to the MFMA streaming kernel), with NKVX_ROTF_P16 row pairs per thread
 //                     and NKVX_ROTF_U16 columns in flight.
@@ -271,7 +274,8 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
                                                         int j, const double* __restrict__ f,
                                                         const double* __restrict__ w, int64_t sv,
                                                         int tiles_per_field,
-                                                        double* __restrict__ partials, int B) {
+                                                        double* __restrict__ partials, int B, int t_lo = 0,
+                                                        int accum = 0) {
     constexpr int kTile = kThreads * kPairs * 2;
     extern __shared__ double red[];  // [4 waves][j]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
     __syncthreads();
 
     const int64_t fb = (int64_t)blockIdx.y * sv;
-    for (int t = blockIdx.x; t < tiles_per_field; t += gridDim.x) {
+    for (int t = t_lo + blockIdx.x; t < tiles_per_field; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 wf[kPairs];
 #pragma unroll
@@ -336,8 +340,10 @@ __global__ __launch_bounds__(kThreads) void k_block_dot(const double* __restrict
     }
     __syncthreads();
     const int b = blockIdx.y * gridDim.x + blockIdx.x;
-    for (int c = threadIdx.x; c < j; c += kThreads)
-        partials[(int64_t)c * B + b] = (red[c] + red[j + c]) + (red[2 * j + c] + red[3 * j + c]);
+    for (int c = threadIdx.x; c < j; c += kThreads) {
+        const double v = (red[c] + red[j + c]) + (red[2 * j + c] + red[3 * j + c]);
+        partials[(int64_t)c * B + b] = accum ? partials[(int64_t)c * B + b] + v : v;
+    }
 }
 
 // Second stage: out[c] = sum_b partials[c][b] in a fixed order (+ replicated time term).
@@ -374,9 +380,11 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
                                                            int tiles_per_field, int tiles_w,
                                                            int tiles_total, int64_t time_off,
                                                            int do_time,
-                                                           double* __restrict__ partials) {
+                                                           double* __restrict__ partials, int t_lo = 0,
+                                                           int t_hi = -1, int accum = 0) {
     constexpr int kTile = kThreads * kPairs * 2;
     __shared__ double lds4[4];
+    if (t_hi < 0) t_hi = tiles_total;
     // time slot (one double): wave 0 of block 0, lanes split the columns.
     if (do_time && blockIdx.x == 0 && threadIdx.x < 64) {
         double s = 0.0;
@@ -385,7 +393,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
         if (threadIdx.x == 0) f[time_off] = OVERWRITE ? s : f[time_off] - s;
     }
     double nrm = 0.0;
-    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+    for (int t = t_lo + blockIdx.x; t < t_hi; t += gridDim.x) {
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 acc[kPairs];
 #pragma unroll
@@ -434,7 +442,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
     }
     if (NORM) {
         nrm = block_sum(nrm, lds4);
-        if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+        if (threadIdx.x == 0) partials[blockIdx.x] = accum ? partials[blockIdx.x] + nrm : nrm;
     }
 }
 
@@ -1535,10 +1543,17 @@ int launch_block_dot_p(const nkv_layout* L, const double* w, const double* Q, in
     if (bx < 1) bx = 1;
     const int B = bx * L->n_wf;
     double* part = partials_of(ws);
+#ifndef NKVX_BD_ROUNDS
+#define NKVX_BD_ROUNDS 0
+#endif
     if (tpf > 0) {
-        hipLaunchKernelGGL(k_block_dot<P>, dim3(bx, L->n_wf), dim3(kThreads), 4 * j * sizeof(double), st,
-                           Q, ld, j, f, w, L->sv, tpf, part, B);
-        NKV_LAUNCHED();
+        const int band = (NKVX_BD_ROUNDS > 0 && tpf >= 2 * NKVX_BD_ROUNDS * bx) ? NKVX_BD_ROUNDS * bx : tpf;
+        for (int lo = 0; lo < tpf; lo += band) {
+            const int hi = lo + band < tpf ? lo + band : tpf;
+            hipLaunchKernelGGL(k_block_dot<P>, dim3(bx, L->n_wf), dim3(kThreads), 4 * j * sizeof(double), st,
+                               Q, ld, j, f, w, L->sv, hi, part, B, lo, lo > 0 ? 1 : 0);
+            NKV_LAUNCHED();
+        }
     }
     const int64_t T = rows_of(L);
     const bool tdot = (flags & NKV_TIME) && L->rank0;
@@ -1564,20 +1579,31 @@ int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q,
     const int tpf = (int)(L->sv / kTile);
     const int tiles_w = tpf * L->n_wf;
     const int tiles_total = (int)(rows_of(L) / kTile);
-    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+#ifndef NKVX_BU_G
+#define NKVX_BU_G kMaxBlocks
+#endif
+#ifndef NKVX_BU_ROUNDS
+#define NKVX_BU_ROUNDS 0
+#endif
+    int g = tiles_total < NKVX_BU_G ? tiles_total : NKVX_BU_G;
     if (g < 1) g = 1;
     *g_out = g;
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;
-    if (over && norm)
-        hipLaunchKernelGGL((k_block_update<true, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (over)
-        hipLaunchKernelGGL((k_block_update<true, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (norm)
-        hipLaunchKernelGGL((k_block_update<false, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else
-        hipLaunchKernelGGL((k_block_update<false, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    NKV_LAUNCHED();
+    const int band = (NKVX_BU_ROUNDS > 0 && tiles_total >= 2 * NKVX_BU_ROUNDS * g) ? NKVX_BU_ROUNDS * g : tiles_total;
+    for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {
+        const int hi = lo + band < tiles_total ? lo + band : tiles_total;
+        const int d0 = lo == 0 ? dt : 0, ac = lo > 0 ? 1 : 0;
+        if (over && norm)
+            hipLaunchKernelGGL((k_block_update<true, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, d0, part, lo, hi, ac);
+        else if (over)
+            hipLaunchKernelGGL((k_block_update<true, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, d0, part, lo, hi, ac);
+        else if (norm)
+            hipLaunchKernelGGL((k_block_update<false, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, d0, part, lo, hi, ac);
+        else
+            hipLaunchKernelGGL((k_block_update<false, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, d0, part, lo, hi, ac);
+        NKV_LAUNCHED();
+    }
     return NKV_OK;
 }
 

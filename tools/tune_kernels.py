@@ -88,6 +88,13 @@ VARIANTS = {
     "x_rf16_p2u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 2, "NKVX_ROTF_U16": 2},
     "x_rf16_p1u8": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 1, "NKVX_ROTF_U16": 8},
     "x_rf16_p4u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 4, "NKVX_ROTF_U16": 2},
+    "x_bd_r1": {"src": "exp", "NKVX_BD_ROUNDS": 1},
+    "x_bd_r2": {"src": "exp", "NKVX_BD_ROUNDS": 2},
+    "x_bd_r4": {"src": "exp", "NKVX_BD_ROUNDS": 4},
+    "x_bu_g768_r1": {"src": "exp", "NKVX_BU_G": 768, "NKVX_BU_ROUNDS": 1},
+    "x_bu_g768_r2": {"src": "exp", "NKVX_BU_G": 768, "NKVX_BU_ROUNDS": 2},
+    "x_bu_g1024_r1": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 1},
+    "x_bu_g1024_r2": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 2},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
