@@ -1,7 +1,8 @@
 """Sharded (world_size 2) GPU path on ONE MI355X: two ranks share the device and exchange partial
 dots through gloo (RCCL cannot place two ranks on one GPU; on an 8-GPU node the same code runs over
 RCCL/xGMI).  Sharded Krylov–Schur must reproduce the single-rank result: identical restart
-trajectory, Ritz values to 1e-12 (SURVEY.md §8(e) gate)."""
+trajectory, Ritz values to 1e-12 (SURVEY.md §8(e) gate) — and the oracle's unsharded Krylov–Schur on
+the same problems (restart trajectory identical, Ritz values to 1e-10)."""
 import os
 import socket
 import sys
@@ -11,6 +12,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+from helpers import match_ritz, ritz_compare_set
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
@@ -91,6 +94,47 @@ def test_ranks_match_one_rank(gpu, world, E_box, E_cyl):
             sel = sorted(set(sel))
             assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) < 1e-12
             np.testing.assert_array_equal(out[(world, 0)][key][4], H2)  # identical H on every rank
+    # and against the oracle (the reference's MGS2 Krylov–Schur restated on the CPU, unsharded):
+    # restart trajectory identical, Ritz values of the comparison set to 1e-10
+    ref = _oracle_ks(E_box, E_cyl)
+    for key in ("lap", "rot"):
+        v2, _r2, m2, c2, _H2 = out[(world, 0)][key]
+        assert m2 == ref[key]["mstart"] and c2 == ref[key]["schur_cnt"], (key, m2, ref[key]["mstart"])
+        sel = ritz_compare_set(ref[key]["vals"], ref[key]["residual"], 1e-6)
+        got = match_ritz(ref[key]["vals"][sel], v2)
+        assert np.max(np.abs(got - ref[key]["vals"][sel]) / np.abs(ref[key]["vals"][sel])) <= 1e-10
+
+
+_ORACLE = {}
+
+
+def _oracle_ks(E_box, E_cyl):
+    """The oracle's Krylov–Schur on the unsharded problems of _run_ks (same operators, seeds,
+    k_dim and schur_tgt)."""
+    if (E_box, E_cyl) in _ORACLE:
+        return _ORACLE[(E_box, E_cyl)]
+    import oracle as orc
+    from helpers import olayout, oracle_diag_matvec, oracle_rot2_matvec
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import box3d_layout, cylinder_layout
+
+    res = {}
+    orc.set_threads(8)
+    try:
+        lay = box3d_layout(E_box)
+        L, w = olayout(lay), syn.mass_weights(lay)
+        d, _ = syn.laplacian_shift_invert(lay)
+        q1 = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 11)))
+        res["lap"] = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 32, 4)
+        lay2 = cylinder_layout(E_cyl)
+        L2, w2 = olayout(lay2), syn.mass_weights(lay2)
+        c, s_, dr, _ = syn.rot2_operator(lay2)
+        q2 = orc.prepare_seed(L2, w2, syn.to_reference_order(lay2, syn.hash_vector(lay2, 5)))
+        res["rot"] = orc.krylov_schur(L2, w2, oracle_rot2_matvec(lay2, c, s_, dr), q2, 24, 2)
+    finally:
+        orc.set_threads(1)
+    _ORACLE[(E_box, E_cyl)] = res
+    return res
 
 
 _RCCL_SCRIPT = r'''
