@@ -24,6 +24,8 @@ pytestmark = pytest.mark.gpu
 LAYOUTS = {
     "2d": NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300),
     "3d_scalar": NekLayout(ldim=3, lx1=5, lx2=3, nelgv=37, n_scalars=1),  # odd sizes, ragged pads
+    "2d_nopr": NekLayout(ldim=2, lx1=6, lx2=4, nelgv=150, ifpo=False),   # no pressure segment (.not. ifpo)
+    "3d_noscal": NekLayout(ldim=3, lx1=4, lx2=2, nelgv=61),              # three weighted fields
 }
 
 
@@ -469,7 +471,9 @@ def test_empty_shard(gpu):
 # ---- DCGS2 entry points, each against numpy on the same inputs (small- and large-tile paths) ----
 from nekstab_next_amd.layout import box3d_layout  # noqa: E402
 
-DC_LAYOUTS = {"small": LAYOUTS["3d_scalar"], "large": box3d_layout(4000)}  # large: >= 2048 4096-row tiles
+DC_LAYOUTS = {"small": LAYOUTS["3d_scalar"], "large": box3d_layout(4000),   # large: >= 2048 4096-row tiles
+              # large tiles with three weighted fields and no pressure segment (.not. ifpo)
+              "large_3f_nopr": NekLayout(ldim=3, lx1=8, lx2=6, nelgv=6000, ifpo=False)}
 
 
 def _wfull(lay, w):
