@@ -6,6 +6,9 @@
 //   NKVX_BD_ROUNDS=R  the single-vector multi-dot (CGS2 passes, closing re-orthogonalisation) as one
 //                     launch per R grid-stride rounds (band partials accumulated per block).
 //   NKVX_BU_ROUNDS=R / NKVX_BU_G=G  the block update (f -= Q h, optional norm partial) likewise.
+//   NKVX_ROTS_B128=1  the MFMA streaming rotation reads its V operands from a permuted, bank-conflict-free
+//                     LDS image with ds_read_b128 (the default layout's reads merge into ds_read2_b64,
+//                     8 LDS-bank-conflict cycles per read: profiles/r02aa_rotate_pmc.json).
 //   NKVX_ROTF16=1     the few-column restart rotation also for 9..16 kept columns (the product sends
 //                     those to the MFMA streaming kernel), with NKVX_ROTF_P16 row pairs per thread
 //                     and NKVX_ROTF_U16 columns in flight.
@@ -1267,6 +1270,20 @@ __global__ __launch_bounds__(kThreads) void k_rotate_mfma(double* __restrict__ Q
 // tile, so each column is read in WAVES*NB*128-byte runs.  LDS: Vs[c * kp + i], kp = 2 (mod 32)
 // doubles: the two 16-lane k-rows of a ds_read_b64 land on disjoint bank pairs.
 // ------------------------------------------------------------------------------------------
+#ifndef NKVX_ROTS_B128
+#define NKVX_ROTS_B128 0
+#endif
+// NKVX_ROTS_B128 LDS image of V: row c (output column) holds 4 sub-rows (one per lk = i mod 4) of
+// PL doubles, V[c][4t + lk] at c*RS + lk*PL + t, so a lane's U A-operands of a k-batch are
+// contiguous (U/2 ds_read_b128); PL, RS chosen so the 16-lane b128 groups hit 16 distinct 16-B
+// slots: PL = 0 mod 32 with RS/2 odd, or PL = 2 mod 4 with RS = 4 mod 8 (the smaller RS).
+__host__ __device__ inline void rots_layout(int k, int U, int* PL, int* RS) {
+    const int kq = ((k + 4 * U - 1) / (4 * U)) * U;   // doubles per sub-row before padding
+    const int pa = (kq + 31) & ~31, ra = 4 * pa + 2;
+    const int pb = kq + ((2 - kq % 4) + 4) % 4, rb = 4 * pb + 4;
+    if (ra <= rb) { *PL = pa; *RS = ra; } else { *PL = pb; *RS = rb; }
+}
+
 template <int NB, int MB, int WAVES, int U>
 __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict__ Q, int64_t ld, int k,
                                                               const double* __restrict__ V, int ldv, int n_out,
@@ -1274,6 +1291,16 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     extern __shared__ __attribute__((aligned(16))) double Vs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
+#if NKVX_ROTS_B128
+    int PL, RS;
+    rots_layout(k, U, &PL, &RS);
+    for (int e = threadIdx.x; e < MB * 16 * RS; e += WAVES * 64) {
+        const int c = e / RS, r = e % RS, q = r / PL, t = r % PL, i = 4 * t + q;
+        Vs[e] = (q < 4 && i < k && c < n_out) ? V[i + (int64_t)c * ldv] : 0.0;
+    }
+    __syncthreads();
+    const double* vs = Vs + lr * RS + lk * PL;
+#else
     // Vs[c][i] for c < 16*MB, i < kp (zero beyond n_out / k: the last 4U-step batch needs no guard)
     for (int e = threadIdx.x; e < MB * 16 * kp; e += WAVES * 64) {
         const int c = e / kp, i = e % kp;
@@ -1281,6 +1308,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     }
     __syncthreads();
     const double* vs = Vs + lr * kp + lk;
+#endif
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t row0 = (tile * WAVES + wave) * (NB * 16);
         const double* q = Q + row0 + lr;
@@ -1298,6 +1326,22 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) b[u][nb] = i < k ? qi[nb * 16] : 0.0;
             }
+#if NKVX_ROTS_B128
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                double2 a2[U / 2];
+                const double2* va = reinterpret_cast<const double2*>(vs + m * 16 * RS + i0 / 4);
+#pragma unroll
+                for (int q = 0; q < U / 2; ++q) a2[q] = va[q];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const double a = (u & 1) ? a2[u >> 1].y : a2[u >> 1].x;
+#pragma unroll
+                    for (int nb = 0; nb < NB; ++nb)
+                        acc[nb][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u][nb], acc[nb][m], 0, 0, 0);
+                }
+            }
+#else
 #pragma unroll
             for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -1308,6 +1352,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
                         acc[nb][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u][nb], acc[nb][m], 0, 0, 0);
                 }
             }
+#endif
         }
 #pragma unroll
         for (int m = 0; m < MB; ++m) {
@@ -2216,7 +2261,12 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
         }
     }
     if (NKV_ROT_STREAM && rows_of(L) % ((int64_t)NKV_ROT_WAVES * NKV_ROT_NB * 16) == 0) {
+#if NKVX_ROTS_B128
+        int PL, kp;
+        rots_layout(k, NKV_ROT_U, &PL, &kp);
+#else
         const int kp = ((k + 31) & ~31) + 2;
+#endif
         const int nact = (n_out + 15) / 16;
         const size_t lds = (size_t)nact * 16 * kp * sizeof(double);
         if (lds <= 160 * 1024) {

@@ -95,6 +95,7 @@ VARIANTS = {
     "x_bu_g768_r2": {"src": "exp", "NKVX_BU_G": 768, "NKVX_BU_ROUNDS": 2},
     "x_bu_g1024_r1": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 1},
     "x_bu_g1024_r2": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 2},
+    "x_rs_b128": {"src": "exp", "NKVX_ROTS_B128": 1},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
@@ -207,6 +208,8 @@ def run(names, E, rounds, js, only=None):
                           8.0 * (j + min(12, j)) * N),
             "rotate_16": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(16, j), st),
                           8.0 * (j + min(16, j)) * N),
+            "rotate_32": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(32, j), st),
+                          8.0 * (j + min(32, j)) * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
         }
