@@ -143,6 +143,10 @@ def run(names, E, rounds, js, only=None):
     Lc = lay.c_struct()
     ldpad = int(os.environ.get("NKV_TUNE_LDPAD", "0"))   # extra doubles of column stride (multiple of 4096,
     # or any even number with the "ldany" build)
+    svpad = int(os.environ.get("NKV_TUNE_SVPAD", "0"))   # extra 4096-row tiles per field segment (field stride)
+    if svpad:
+        Lc.sv += 4096 * svpad
+        Lc.ld = -(-(Lc.n_wf * Lc.sv + Lc.sp + 1) // 4096) * 4096
     Lc.ld += ldpad
     Lp = ctypes.byref(Lc)
     Q = torch.empty((jmax + 1, Lc.ld), dtype=torch.float64, device=dev)
@@ -150,9 +154,9 @@ def run(names, E, rounds, js, only=None):
     st = torch.cuda.current_stream().cuda_stream
     for i in range(jmax + 1):
         _lib.check(lib0.nkv_fill_hash(Lp, Q[i].data_ptr(), 100 + i, 0, 0, st), "fill")
-    f = torch.empty(lay.ld, dtype=torch.float64, device=dev)
+    f = torch.empty(Lc.ld, dtype=torch.float64, device=dev)
     _lib.check(lib0.nkv_fill_hash(Lp, f.data_ptr(), 5, 0, 0, st), "fill")
-    w = torch.zeros(lay.sv, dtype=torch.float64, device=dev)
+    w = torch.zeros(Lc.sv, dtype=torch.float64, device=dev)
     w[: lay.n_v] = torch.as_tensor(syn.mass_weights(lay)).to(dev)
     ws = torch.zeros((lib0.nkv_workspace_bytes(Lp, jmax + 1) + 7) // 8 + 4096 * (jmax + 2), dtype=torch.float64, device=dev)
     h = torch.full((jmax + 1,), 1e-3, dtype=torch.float64, device=dev)
@@ -161,8 +165,8 @@ def run(names, E, rounds, js, only=None):
     N, Nw, nv = lay.N, lay.N_w, lay.n_v
     V = torch.eye(jmax, dtype=torch.float64, device=dev).flatten()  # rotation by I keeps Q bounded
     hd = torch.zeros(2 * (jmax + 1), dtype=torch.float64, device=dev)
-    f2 = torch.zeros(lay.ld, dtype=torch.float64, device=dev)
-    dgl = torch.full((lay.ld,), 0.5, dtype=torch.float64, device=dev)
+    f2 = torch.zeros(Lc.ld, dtype=torch.float64, device=dev)
+    dgl = torch.full((Lc.ld,), 0.5, dtype=torch.float64, device=dev)
     nrm1 = torch.ones(8, dtype=torch.float64, device=dev)
     coefs = {}
     for jj in js:   # DCGS2 coefficients for m = jj-1: small x, y, a; rinv = s = 1 (vectors stay bounded)
