@@ -9,7 +9,9 @@
  * 3-D lx1=8 layout with one scalar (E elements), diagonal synthetic operator, seed from
  * nkv_fill_hash, m DCGS2 Arnoldi steps (single rank: the all-reduces of INTEGRATION.md §2b are the
  * identity), the closing re-orthogonalisation, then checks of W-orthonormality of the basis and of
- * the Arnoldi relation A Q_m = Q_{m+1} H through the same ABI.  Exit status 0 on success.
+ * the Arnoldi relation A Q_m = Q_{m+1} H through the same ABI; then the same factorisation as ONE
+ * call of the native driver nkv_arnoldi_dcgs2 (the operator as a callback), which must reproduce
+ * Q and H bit for bit.  Exit status 0 on success.
  */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -37,6 +39,18 @@
     } while (0)
 
 static int64_t roundup(int64_t n, int64_t m) { return (n + m - 1) / m * m; }
+
+/* the operator as a callback of nkv_arnoldi_dcgs2 (a Fortran host passes c_funloc of a bind(C)
+   procedure wrapping its time-stepper) */
+typedef struct {
+    const nkv_layout* L;
+    const double* d;
+} diag_op;
+
+static int diag_matvec(void* user, const double* x, double* y, void* stream) {
+    const diag_op* op = (const diag_op*)user;
+    return nkv_op_diag(op->L, op->d, x, y, 0.0, stream);
+}
 
 int main(int argc, char** argv) {
     const int E = argc > 1 ? atoi(argv[1]) : 512;
@@ -135,7 +149,33 @@ int main(int argc, char** argv) {
     }
     printf("arnoldi_c: N=%lld m=%d  max|Q^T W Q - I| = %.3e  max ||A q - Q h|| / max|H| = %.3e  H(m+1,m) = %.6e\n",
            (long long)(L.n_wf * L.n_v + L.n_p), m, orth, arn / hmax, H[(int64_t)(m - 1) * (m + 1) + m]);
-    const int ok = orth < 1e-12 && arn / hmax < 1e-12;
+
+    /* the same factorisation as ONE call of the native driver (operator as a callback, no
+       all-reduce on one rank): Q and H must equal the step-by-step loop's bit for bit */
+    double *Q2, *Hd2, *scr;
+    HK(hipMalloc((void**)&Q2, (size_t)(m + 1) * vbytes));
+    HK(hipMalloc((void**)&Hd2, (size_t)m * (m + 1) * sizeof(double)));
+    HK(hipMalloc((void**)&scr, nkv_arnoldi_scratch_doubles(m) * sizeof(double)));
+    HK(hipMemsetAsync(Q2, 0, (size_t)(m + 1) * vbytes, st));
+    HK(hipMemsetAsync(Hd2, 0, (size_t)m * (m + 1) * sizeof(double), st));
+    CK(nkv_fill_hash(&L, Q2, 11, 0, 0, st));
+    CK(nkv_dot(&L, w, Q2, Q2, nrm, ws, 0, st));
+    CK(nkv_normalize_dev(&L, Q2, nrm, NULL, 0, st));
+    diag_op op = {&L, d};
+    CK(nkv_arnoldi_dcgs2(&L, w, Q2, 1, m, Hd2, m + 1, f, scr, ws, diag_matvec, &op, NULL, NULL, 0, st));
+    double* H2 = (double*)malloc((size_t)m * (m + 1) * sizeof(double));
+    double *qa = (double*)malloc(vbytes), *qb = (double*)malloc(vbytes);
+    HK(hipMemcpyAsync(H2, Hd2, (size_t)m * (m + 1) * sizeof(double), hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    int same = memcmp(H, H2, (size_t)m * (m + 1) * sizeof(double)) == 0;
+    for (int c = 0; c <= m && same; ++c) {
+        HK(hipMemcpy(qa, Q + (int64_t)c * L.ld, vbytes, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(qb, Q2 + (int64_t)c * L.ld, vbytes, hipMemcpyDeviceToHost));
+        same = memcmp(qa, qb, vbytes) == 0;
+    }
+    printf("arnoldi_c: nkv_arnoldi_dcgs2 (one call) %s the step-by-step loop\n",
+           same ? "equals bit for bit" : "DIFFERS from");
+    const int ok = orth < 1e-12 && arn / hmax < 1e-12 && same;
     printf(ok ? "arnoldi_c: OK\n" : "arnoldi_c: FAILED\n");
     (void)rows;
     return ok ? 0 : 1;

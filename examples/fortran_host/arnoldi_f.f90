@@ -2,12 +2,29 @@
 ! the replacement of arnoldi_factorization / update_hessenberg_matrix (krylov_decomposition.f90)
 ! by the loop of INTEGRATION.md §2b on one rank (gop = identity), then W-orthonormality and the
 ! Arnoldi relation A Q_m = Q_{m+1} H checked through the same calls.   usage: arnoldi_f [E [m]]
-program arnoldi_f
+module diag_callback
+   ! the operator handed to nkv_arnoldi_dcgs2 as a callback: y = d .* x on the library's stream
    use iso_c_binding
    use nkv_bindings
    implicit none
+   type(nkv_layout), save :: Lcb
+   type(c_ptr), save :: dcb
+contains
+   integer(c_int) function diag_mv(user, x, y, stream) bind(C)
+      type(c_ptr), value :: user, x, y, stream
+      diag_mv = nkv_op_diag(Lcb, dcb, x, y, 0.0d0, stream)
+   end function diag_mv
+end module diag_callback
+
+program arnoldi_f
+   use iso_c_binding
+   use nkv_bindings
+   use diag_callback
+   implicit none
    type(nkv_layout), target :: L
-   type(c_ptr) :: Q, f, d, w, Hdev, hv, coef, nrm, hcol, ws, st, u
+   type(c_ptr) :: Q, f, d, w, Hdev, hv, coef, nrm, hcol, ws, st, u, Q2, H2dev, scr
+   real(c_double), allocatable, target :: H2(:, :), qa(:), qb(:)
+   logical :: same
    integer :: E, m, j, c, r, nargs
    character(len=32) :: arg
    integer(c_size_t) :: vbytes, wsb
@@ -96,7 +113,32 @@ program arnoldi_f
    end do
    print '(a,i0,a,i0,a,es10.3,a,es10.3,a,es14.6)', 'arnoldi_f: N=', L%n_wf*L%n_v + L%n_p, ' m=', m, &
       '  max|Q^T W Q - I| = ', orth, '  max||A q - Q h||/max|H| = ', arn/hmax, '  H(m+1,m) = ', H(m + 1, m)
-   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12) then
+   ! the same factorisation as ONE native call, the operator a Fortran callback: bit-identical
+   call ck(hipMalloc(Q2, (m + 1)*vbytes), 'hipMalloc Q2')
+   call ck(hipMalloc(H2dev, int(m*(m + 1), c_size_t)*8), 'hipMalloc H2')
+   call ck(hipMalloc(scr, nkv_arnoldi_scratch_doubles(int(m, c_int))*8), 'hipMalloc scratch')
+   call ck(hipMemset(Q2, 0, (m + 1)*vbytes), 'memset Q2')
+   call ck(hipMemset(H2dev, 0, int(m*(m + 1), c_size_t)*8), 'memset H2')
+   call ck(nkv_fill_hash(L, Q2, 11_c_int64_t, 0_c_int64_t, 0_c_int64_t, st), 'seed 2')
+   call ck(nkv_dot(L, w, Q2, Q2, nrm, ws, 0, st), 'seed norm 2')
+   call ck(nkv_normalize_dev(L, Q2, nrm, c_null_ptr, 0, st), 'normalise 2')
+   Lcb = L; dcb = d
+   call ck(nkv_arnoldi_dcgs2(L, w, Q2, 1, int(m, c_int), H2dev, int(m + 1, c_int64_t), f, scr, ws, &
+                             c_funloc(diag_mv), c_null_ptr, c_null_funptr, c_null_ptr, 0, st), 'arnoldi_dcgs2')
+   allocate (H2(m + 1, m), qa(L%ld), qb(L%ld))
+   call ck(hipMemcpy(c_loc(H2), H2dev, int(m*(m + 1), c_size_t)*8, hipMemcpyDeviceToHost), 'H2 down')
+   same = all(H2 == H)
+   do c = 0, m
+      call ck(hipMemcpy(c_loc(qa), col(Q, c, L%ld), vbytes, hipMemcpyDeviceToHost), 'q down')
+      call ck(hipMemcpy(c_loc(qb), col(Q2, c, L%ld), vbytes, hipMemcpyDeviceToHost), 'q2 down')
+      same = same .and. all(qa == qb)
+   end do
+   if (same) then
+      print '(a)', 'arnoldi_f: nkv_arnoldi_dcgs2 (one call, Fortran callback) equals the step-by-step loop bit for bit'
+   else
+      print '(a)', 'arnoldi_f: nkv_arnoldi_dcgs2 DIFFERS from the step-by-step loop'
+   end if
+   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12 .and. same) then
       print '(a)', 'arnoldi_f: OK'
    else
       print '(a)', 'arnoldi_f: FAILED'

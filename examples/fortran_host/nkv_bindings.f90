@@ -88,6 +88,21 @@ module nkv_bindings
          type(c_ptr), value :: w, Q, coef, qj, win, fout, nrm2, ws, stream
          integer(c_int), value :: m, flags
       end function
+      ! the whole DCGS2 factorisation in one call (replaces `call arnoldi_factorization(...)`);
+      ! matvec / allreduce are c_funloc's of bind(C) procedures (allreduce: c_null_funptr on one rank)
+      integer(c_size_t) function nkv_arnoldi_scratch_doubles(m) bind(C, name="nkv_arnoldi_scratch_doubles")
+         import :: c_size_t, c_int
+         integer(c_int), value :: m
+      end function
+      integer(c_int) function nkv_arnoldi_dcgs2(L, w, Q, mstart, mend, H, ldh, f, scratch, ws, matvec, mv_user, &
+            allreduce, ar_user, flags, stream) bind(C, name="nkv_arnoldi_dcgs2")
+         import :: c_int, c_int64_t, c_ptr, c_funptr, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: w, Q, H, f, scratch, ws, mv_user, ar_user, stream
+         integer(c_int), value :: mstart, mend, flags
+         integer(c_int64_t), value :: ldh
+         type(c_funptr), value :: matvec, allreduce
+      end function
       ! HIP runtime (device memory for the host's arrays)
       integer(c_int) function hipMalloc(p, bytes) bind(C, name="hipMalloc")
          import :: c_int, c_ptr, c_size_t

@@ -56,8 +56,8 @@ extern "C" {
  * live in LDS (64 B per column for the two-vector dot).  The reference's k_dim defaults to 100
  * (main.f90:9); GMRES on the cylinder uses 200 (1cyl.usr:14). */
 #define NKV_MAX_COLS 1024
-/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols with more than 8 output
- * columns): a Krylov–Schur restart keeping more than 8 vectors and the materialisation of a lazy
+/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols with more than 16 output
+ * columns): a Krylov–Schur restart keeping more than 16 vectors and the materialisation of a lazy
  * DCGS2 basis, so those need k_dim <= 576. */
 #define NKV_ROT_MAX_K 576
 
@@ -185,6 +185,30 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
                      double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream);
 
+/* ---- the whole factorisation natively (a8: arnoldi_factorization, krylov_decomposition.f90:2-99 —
+ * the loop :68-96 calling matvec then update_hessenberg_matrix) as ONE call: the DCGS2 sequence
+ * above for mstep = mstart..mend, then the closing re-orthogonalisation, orchestrated in C++ (the
+ * same entry points in the same order as nekstab_next_amd/arnoldi.py, so the results are identical
+ * bit for bit).  For a Fortran/C host that replaces `call arnoldi_factorization(Q, H, mstart, mend,
+ * ksize)` without a Python layer.
+ *   On entry columns 0..mstart-1 of Q are final and W-orthonormal (column mstart-1: the normalised
+ *   seed, or Q(k+1) moved to Q(mstart) by a Krylov–Schur restart) and H columns 0..mstart-2 hold the
+ *   factorisation so far (row mstart-1 the restart row).  On return Q columns 0..mend and H columns
+ *   0..mend-1 form an Arnoldi factorisation A Q_mend = Q_{mend+1} H.
+ *   H_dev: device, column-major, leading dimension ldh >= mend+1.  f: one device vector (scratch).
+ *   scratch_dev: nkv_arnoldi_scratch_doubles(mend) doubles of device memory; ws as for the dots.
+ *   matvec(mv_user, x, y, stream): y = A x for device vectors x, y, enqueued on `stream`; returns 0.
+ *   allreduce(ar_user, buf, n, stream): in-place SUM of n device doubles over the ranks, ordered on
+ *   `stream` (ncclAllReduce on it, or a stream sync + MPI_Allreduce); NULL on a single rank.
+ *   flags: NKV_TIME_DOT includes the time products in the dots (uparam(1)==2.1, k_dot :52-54).
+ *   A callback's non-zero return stops the factorisation with NKV_EINVAL (see nkv_last_error). */
+typedef int (*nkv_matvec_fn)(void* user, const double* x, double* y, void* stream);
+typedef int (*nkv_allreduce_fn)(void* user, double* buf, int n, void* stream);
+size_t nkv_arnoldi_scratch_doubles(int m);
+int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
+                      int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec, void* mv_user,
+                      nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
+
 /* DCGS2 over a LAZY basis (same replacement target): the finished q_j is never written.  The stored
  * columns S_0..S_{m-1} keep the raw provisional vectors and the orthonormal basis is Q = S T with
  * T upper triangular (device, column c at T + c*ldt, ldt >= m+1; T_0 empty, a finished column's
@@ -213,7 +237,7 @@ int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int l
  * Columns n_out..k-1 are left as they were.  schur_condensation only keeps the mstart selected
  * Schur vectors (eigensolvers.f90:416-459: Q(mstart+1..k) are overwritten by the next
  * factorisation before being read), so the restart calls this with n_out = mstart.
- * k <= NKV_ROT_MAX_K, or k <= NKV_MAX_COLS when n_out <= 8 (the usual restart). */
+ * k <= NKV_ROT_MAX_K, or k <= NKV_MAX_COLS when n_out <= 16 (the usual restart). */
 int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out,
                     void* stream);
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint, c_uint64, c_void_p
+from ctypes import CFUNCTYPE, POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint, c_uint64, c_void_p
 
 import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
 
@@ -55,6 +55,9 @@ class nkv_layout(Structure):
 
 _P = c_void_p  # device pointers and streams travel as plain addresses
 _L = POINTER(nkv_layout)
+# callbacks of nkv_arnoldi_dcgs2: matvec(user, x, y, stream), allreduce(user, buf, n, stream)
+MATVEC_FN = CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p, c_void_p)
+ALLREDUCE_FN = CFUNCTYPE(c_int, c_void_p, c_void_p, c_int, c_void_p)
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
@@ -78,6 +81,9 @@ _SIGNATURES = {
     "nkv_block_dot2": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_dcgs2_coef": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, _P]),
     "nkv_dcgs2_update": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, _P, _P, c_uint, _P]),
+    "nkv_arnoldi_scratch_doubles": (c_size_t, [c_int]),
+    "nkv_arnoldi_dcgs2": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P, ALLREDUCE_FN, _P,
+                                  c_uint, _P]),
     "nkv_combine": (c_int, [_L, _P, c_int, _P, _P, c_uint, _P]),
     "nkv_normalize_store": (c_int, [_L, _P, _P, _P, _P, c_uint, _P]),
     "nkv_mgs2_step": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),

@@ -25,6 +25,9 @@ Two orthogonalisation modes share the rest of the path:
   step later, inside the same passes).  Two reads of Q per step instead of three, no separate
   normalisation pass; the last vector of a factorisation is re-orthogonalised and normalised once
   at the end, so on return Q and H are exactly an Arnoldi factorisation, as with cgs2.
+* ``"dcgs2-native"``: the same DCGS2 sequence orchestrated inside the library by ONE C-ABI call
+  (``nkv_arnoldi_dcgs2``), the operator and the all-reduce passed as callbacks — the entry a
+  Fortran/C host binds to replace ``arnoldi_factorization`` whole; bit-identical to ``"dcgs2"``.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
 
@@ -242,6 +245,52 @@ def _dcgs2_close_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> N
     ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
 
 
+def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int, mend: int,
+                  f: NekVector, transpose: bool) -> None:
+    """The DCGS2 factorisation as ONE library call (``nkv_arnoldi_dcgs2``, include/nekkrylov.h): the
+    C++ side runs the step sequence of ``_dcgs2_step`` / ``_dcgs2_close`` (same entry points, same
+    order, so the result is bit-identical to ``mode="dcgs2"``) and calls back for the operator and
+    the all-reduce — the shape a Fortran host uses to replace ``arnoldi_factorization``."""
+    lib = ctx.lib
+    need = int(lib.nkv_arnoldi_scratch_doubles(mend))
+    scratch = getattr(ctx, "_arnoldi_scratch", None)
+    if scratch is None or scratch.numel() < need:
+        scratch = ctx._arnoldi_scratch = torch.zeros(need, dtype=torch.float64, device=ctx.device)
+    base, ld8, fptr = Q.ptr, 8 * ctx.layout.ld, f.ptr
+    apply = op.rmatvec if transpose else op.matvec
+    errors = []
+
+    def matvec(_user, x, y, _stream):
+        try:
+            c, r = divmod((x or 0) - base, ld8)
+            if r or not 0 <= c < Q.k or y != fptr:
+                raise ValueError(f"nkv_arnoldi_dcgs2 matvec callback: x={x:#x}, y={y} are not a basis column and f")
+            apply(Q[c], f)
+            return 0
+        except BaseException as e:  # noqa: BLE001 — surfaced after the call returns
+            errors.append(e)
+            return 1
+
+    def allreduce(_user, buf, n, _stream):
+        try:
+            if buf != scratch.data_ptr() or not 0 < n <= scratch.numel():
+                raise ValueError("nkv_arnoldi_dcgs2 allreduce callback: unexpected buffer")
+            ctx.comm.allreduce_(scratch[:n])
+            return 0
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+            return 1
+
+    mv_c = _lib.MATVEC_FN(matvec)
+    ar_c = _lib.ALLREDUCE_FN(allreduce) if (ctx.comm.world > 1 or ctx.comm.force) else None
+    rc = lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(mstart), int(mend), Hd.t.data_ptr(), Hd.k + 1,
+                               fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None, ar_c, None,
+                               NKV_TIME_DOT if ctx.time_in_dot else 0, ctx.stream)
+    if errors:
+        raise errors[0]
+    _lib.check(rc, "nkv_arnoldi_dcgs2")
+
+
 def _settle_basis(Q: Basis, mstart: int, lazy: bool) -> None:
     """Before a factorisation from ``mstart``: from 1 only the caller's seed column is read, so any
     lazy state is stale (T = I); otherwise columns < mstart must be usable — final, or (lazy run)
@@ -272,6 +321,14 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         raise ValueError("basis too small")
     if f is None:
         f = ctx.vector()
+    if mode == "dcgs2-native":   # the same DCGS2 sequence, orchestrated by the library (one ABI call)
+        if on_step is None and not lazy:
+            if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+                raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+            _settle_basis(Q, mstart, lazy=False)
+            _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose)
+            return
+        mode = "dcgs2"
     if mode == "dcgs2" and on_step is None:
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")

@@ -1956,6 +1956,51 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
     return NKV_OK;
 }
 
+// ---- the whole DCGS2 factorisation, driven natively (arnoldi_factorization, krylov_decomposition.f90:
+// 2-99: the loop :68-96 with update_hessenberg_matrix replaced by the DCGS2 entry points above).  The
+// host-side orchestration of nekstab_next_amd/arnoldi.py (_dcgs2_step / _dcgs2_close) in C++, for hosts
+// without Python: the caller supplies the operator and the all-reduce as callbacks.
+size_t nkv_arnoldi_scratch_doubles(int m) { return (size_t)(2 * (m + 1) + 4 * m + 16); }
+
+int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
+                      int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec, void* mv_user,
+                      nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    if (!matvec) return fail(NKV_EINVAL, "matvec callback is NULL");
+    if (!H_dev || !scratch_dev) return fail(NKV_EINVAL, "H/scratch is NULL");
+    if (mstart < 1 || mend > NKV_MAX_COLS) return fail(NKV_EINVAL, "steps %d..%d outside 1..%d", mstart, mend, NKV_MAX_COLS);
+    if (mend < mstart) return NKV_OK;
+    if (ldh < mend + 1) return fail(NKV_EINVAL, "ldh=%lld < mend+1=%d", (long long)ldh, mend + 1);
+    const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;   // time products in the dots (k_dot :52-54)
+    double* hd = scratch_dev;                  // [Q^T W u ; Q^T W A u], 2(mend+1)
+    double* coef = scratch_dev + 2 * (mend + 1);
+    auto col = [L, Q](int c) { return Q + (int64_t)c * L->ld; };
+    for (int j = mstart; j <= mend; ++j) {     // step j: column j-1 holds u (normalised at the first step)
+        const int m = j - 1;
+        double* u = col(m);
+        int rc = matvec(mv_user, u, f, stream);
+        if (rc != 0) return fail(NKV_EINVAL, "matvec callback returned %d at step %d", rc, j);
+        CHECK(nkv_block_dot2(L, w, Q, j, u, f, hd, ws, tf | NKV_X_IS_LAST, stream));
+        if (allreduce && (rc = allreduce(ar_user, hd, 2 * j, stream)) != 0)
+            return fail(NKV_EINVAL, "allreduce callback returned %d at step %d", rc, j);
+        CHECK(nkv_dcgs2_coef(m, hd, hd + j, j == mstart ? nullptr : hd + m, H_dev, ldh, coef, ws, stream));
+        CHECK(nkv_dcgs2_update(L, w, Q, m, coef, u, f, col(j), nullptr, ws, NKV_TIME, stream));
+    }
+    // closing re-orthogonalisation and normalisation of the provisional column mend
+    const int m = mend;
+    double* u = col(m);
+    CHECK(nkv_block_dot(L, w, Q, m + 1, u, hd, ws, tf, stream));
+    if (allreduce) {
+        const int rc = allreduce(ar_user, hd, m + 1, stream);
+        if (rc != 0) return fail(NKV_EINVAL, "allreduce callback returned %d (closing step)", rc);
+    }
+    CHECK(nkv_dcgs2_coef(m, hd, nullptr, hd + m, H_dev, ldh, coef, ws, stream));
+    CHECK(nkv_block_update(L, w, Q, m, hd, u, nullptr, ws, NKV_TIME, stream));
+    return nkv_normalize_dev(L, u, coef + 2 * m + 3, nullptr, 0, stream);
+}
+
 int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,
                        int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
                        unsigned flags, void* stream) {

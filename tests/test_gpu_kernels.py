@@ -263,6 +263,57 @@ def test_rotate_cols_row_bands(gpu, n_out):
     np.testing.assert_array_equal(got[n_out:], before[n_out:])
 
 
+@pytest.mark.parametrize("name", list(LAYOUTS) + ["large"])
+def test_native_dcgs2_driver_bit_identical(gpu, name):
+    """nkv_arnoldi_dcgs2 (the whole DCGS2 factorisation in one ABI call, operator as a callback)
+    gives the Python-driven DCGS2 factorisation bit for bit — from the seed and from mstart > 1."""
+    from nekstab_next_amd.layout import box3d_layout
+
+    lay = box3d_layout(4000) if name == "large" else LAYOUTS[name]
+    ctx, _ = make_ctx(lay, max_cols=32)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    m = 20
+    out = {}
+    for mode in ("dcgs2", "dcgs2-native"):
+        Q = ctx.basis(m + 1)
+        Q[0].fill_hash(5)
+        k_normalize(Q[0])
+        Hd = HessenbergDev(ctx, m)
+        arnoldi_factorization(ctx, op, Q, Hd, 1, 12, mode=mode)
+        arnoldi_factorization(ctx, op, Q, Hd, 13, m, mode=mode)   # continue from column 12 (mstart > 1)
+        out[mode] = (Hd.download(), Q.storage.cpu().numpy())
+    np.testing.assert_array_equal(out["dcgs2"][0], out["dcgs2-native"][0])
+    np.testing.assert_array_equal(out["dcgs2"][1], out["dcgs2-native"][1])
+
+
+def test_native_dcgs2_driver_callback_errors(gpu):
+    """A failing operator callback stops nkv_arnoldi_dcgs2 with the callback's exception (Python)
+    and NKV_EINVAL (C ABI); a NULL matvec is refused."""
+    from nekstab_next_amd import _lib as L_
+
+    lay = LAYOUTS["2d"]
+    ctx, _ = make_ctx(lay, max_cols=8)
+    Q = ctx.basis(5)
+    Q[0].fill_hash(3)
+    k_normalize(Q[0])
+    Hd = HessenbergDev(ctx, 4)
+
+    class Boom(DiagOperator):
+        def matvec(self, x, y):
+            raise RuntimeError("operator failed")
+
+    d, _ = syn.diag_spectrum(lay)
+    with pytest.raises(RuntimeError, match="operator failed"):
+        arnoldi_factorization(ctx, Boom(ctx, d), Q, Hd, 1, 4, mode="dcgs2-native")
+    f = ctx.vector()
+    scratch = torch.zeros(int(ctx.lib.nkv_arnoldi_scratch_doubles(4)), dtype=torch.float64, device=ctx.device)
+    rc = ctx.lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, 1, 4, Hd.t.data_ptr(), 5, f.ptr,
+                                   scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(), None, L_.ALLREDUCE_FN(),
+                                   None, 0, ctx.stream)
+    assert rc == L_.NKV_EINVAL and "matvec" in L_.last_error()
+
+
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2", "dcgs2-lazy"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):

@@ -45,7 +45,7 @@ def _seed(ctx, lay, L, w, s=11):
     return seed, q1
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "dcgs2-native"])
 def test_config1_krylov_schur(gpu, mode):
     """Config 1: 2-D lx1=6, E=1136 (N=99,968), diag spectrum, k_dim=16, schur_tgt=5."""
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=1136)
