@@ -282,7 +282,7 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
             return 1
 
     mv_c = _lib.MATVEC_FN(matvec)
-    ar_c = _lib.ALLREDUCE_FN(allreduce) if (ctx.comm.world > 1 or ctx.comm.force) else None
+    ar_c = _lib.ALLREDUCE_FN(allreduce) if (ctx.comm.world > 1 or ctx.comm.force) else _lib.ALLREDUCE_FN()
     rc = lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(mstart), int(mend), Hd.t.data_ptr(), Hd.k + 1,
                                fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None, ar_c, None,
                                NKV_TIME_DOT if ctx.time_in_dot else 0, ctx.stream)
