@@ -574,6 +574,11 @@ def run(args):
                 "launches": ph["launches"],
                 "scope": "one GPU (the only rank)" if world == 1 else
                          f"rank 0's shard on its own GPU (1/{world} of N); peak is one GPU's HBM",
+                # a rank's vector that fits the 256 MiB Infinity Cache (MALL) is partly re-read from
+                # it (the vector one kernel writes is read by the next): not pure HBM traffic
+                "infinity_cache": (None if 8.0 * lay.ld >= 256 * 2 ** 20 else
+                                   f"rank vectors of {8.0 * lay.ld / 2 ** 20:.0f} MiB fit the 256 MiB Infinity "
+                                   "Cache: part of the achieved rate is MALL hits, not HBM"),
             },
             "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                        for k, v in phases.items()},
