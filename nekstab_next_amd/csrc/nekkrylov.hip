@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 // P row pairs of a tile, walks the k columns U at a time with 16-byte non-temporal loads (1 KiB
 // per wave instruction, each column read in kThreads*P*16-byte runs), and keeps NO accumulators
 // per row; V[c, 0:NO] is wave-uniform (scalar loads).  2 N k NO flop against 8 N (k + NO) bytes:
-// at NO <= 8 this is HBM-bound on the VALU, where the MFMA tile would waste 16-NO of its 16
+// at NO <= 16 this is HBM-bound on the VALU, where the MFMA tile would waste 16-NO of its 16
 // output columns and read Q in 128-byte pieces.  All k inputs of a row are consumed before its NO
 // outputs are stored and no other thread touches that row, so in place is safe.
 // ------------------------------------------------------------------------------------------
