@@ -209,6 +209,18 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
                       int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec, void* mv_user,
                       nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
 
+/* update_hessenberg_matrix(H, f, Q, k) itself as one call (krylov_decomposition.f90:103-189): the
+ * fused 3-pass CGS2 sequence of the block Gram–Schmidt section above (block_dot, all-reduce,
+ * block_update_dot, all-reduce, block_update + norm, all-reduce, arnoldi_finish) with the
+ * all-reduce as the callback of nkv_arnoldi_dcgs2 (NULL on one rank).  f is orthogonalised twice
+ * against Q[:,0:j] (W inner product), q_out = f/||f||_W, hcol_dev[0:j+1] = H(1:k+1, k).  j = 0
+ * only normalises.  scratch_dev: nkv_arnoldi_scratch_doubles(j) doubles.  flags: NKV_TIME_DOT
+ * (time products in the dots).  For per-column consumers (GMRES: newton_krylov.f90:252) and
+ * checkpointing Arnoldi, where each column must be final when its step returns. */
+int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
+                          double* hcol_dev, double* scratch_dev, void* ws, nkv_allreduce_fn allreduce, void* ar_user,
+                          unsigned flags, void* stream);
+
 /* DCGS2 over a LAZY basis (same replacement target): the finished q_j is never written.  The stored
  * columns S_0..S_{m-1} keep the raw provisional vectors and the orthonormal basis is Q = S T with
  * T upper triangular (device, column c at T + c*ldt, ldt >= m+1; T_0 empty, a finished column's

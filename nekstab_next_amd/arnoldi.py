@@ -28,6 +28,8 @@ Two orthogonalisation modes share the rest of the path:
 * ``"dcgs2-native"``: the same DCGS2 sequence orchestrated inside the library by ONE C-ABI call
   (``nkv_arnoldi_dcgs2``), the operator and the all-reduce passed as callbacks — the entry a
   Fortran/C host binds to replace ``arnoldi_factorization`` whole; bit-identical to ``"dcgs2"``.
+* ``"cgs2-native"``: the ``"cgs2"`` step as ONE library call per column (``nkv_update_hessenberg``,
+  the reference's ``update_hessenberg_matrix`` entry), the all-reduce as a callback.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
 
@@ -80,6 +82,16 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
     projection coefficients h1+h2 go to hcol[0:j] and ||f|| to hcol[j] (device memory).  j = 0
     only normalises."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    if mode == "cgs2-native":   # the same CGS2 sequence as ONE library call (nkv_update_hessenberg)
+        scratch = _native_scratch(ctx, j)
+        errors = []
+        ar_c = _allreduce_callback(ctx, scratch, errors)
+        rc = ctx.lib.nkv_update_hessenberg(ctx._Lp, w, Q.ptr, int(j), f.ptr, out_ptr, hcol_ptr, scratch.data_ptr(), ws,
+                                           ar_c, None, NKV_TIME_DOT if ctx.time_in_dot else 0, st)
+        if errors:
+            raise errors[0]
+        _lib.check(rc, "nkv_update_hessenberg")
+        return
     if j == 0:
         tf = NKV_TIME if ctx.time_in_dot else 0
         nrm = ctx.scal[3:4]
@@ -245,6 +257,36 @@ def _dcgs2_close_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> N
     ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
 
 
+def _native_scratch(ctx: NekContext, m: int) -> torch.Tensor:
+    """Device scratch of the one-call drivers (nkv_arnoldi_scratch_doubles), kept on the context."""
+    need = int(ctx.lib.nkv_arnoldi_scratch_doubles(max(int(m), ctx.max_cols)))
+    scratch = getattr(ctx, "_arnoldi_scratch", None)
+    if scratch is None or scratch.numel() < need:
+        scratch = ctx._arnoldi_scratch = torch.zeros(need, dtype=torch.float64, device=ctx.device)
+    return scratch
+
+
+def _allreduce_callback(ctx: NekContext, scratch: torch.Tensor, errors: list):
+    """The all-reduce callback of the one-call drivers: in-place SUM of a slice of ``scratch``
+    through the context's communicator (a typed NULL on one rank without forced collectives)."""
+    if not (ctx.comm.world > 1 or ctx.comm.force):
+        return _lib.ALLREDUCE_FN()
+    base, size = scratch.data_ptr(), scratch.numel()
+
+    def allreduce(_user, buf, n, _stream):
+        try:
+            off, r = divmod((buf or 0) - base, 8)
+            if r or off < 0 or n <= 0 or off + n > size:
+                raise ValueError("one-call driver allreduce callback: buffer outside the scratch")
+            ctx.comm.allreduce_(scratch[off:off + n])
+            return 0
+        except BaseException as e:  # noqa: BLE001 — surfaced after the call returns
+            errors.append(e)
+            return 1
+
+    return _lib.ALLREDUCE_FN(allreduce)
+
+
 def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int, mend: int,
                   f: NekVector, transpose: bool) -> None:
     """The DCGS2 factorisation as ONE library call (``nkv_arnoldi_dcgs2``, include/nekkrylov.h): the
@@ -252,10 +294,7 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
     order, so the result is bit-identical to ``mode="dcgs2"``) and calls back for the operator and
     the all-reduce — the shape a Fortran host uses to replace ``arnoldi_factorization``."""
     lib = ctx.lib
-    need = int(lib.nkv_arnoldi_scratch_doubles(mend))
-    scratch = getattr(ctx, "_arnoldi_scratch", None)
-    if scratch is None or scratch.numel() < need:
-        scratch = ctx._arnoldi_scratch = torch.zeros(need, dtype=torch.float64, device=ctx.device)
+    scratch = _native_scratch(ctx, mend)
     base, ld8, fptr = Q.ptr, 8 * ctx.layout.ld, f.ptr
     apply = op.rmatvec if transpose else op.matvec
     errors = []
@@ -264,25 +303,15 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
         try:
             c, r = divmod((x or 0) - base, ld8)
             if r or not 0 <= c < Q.k or y != fptr:
-                raise ValueError(f"nkv_arnoldi_dcgs2 matvec callback: x={x:#x}, y={y} are not a basis column and f")
+                raise ValueError(f"nkv_arnoldi_dcgs2 matvec callback: x={x}, y={y} are not a basis column and f")
             apply(Q[c], f)
             return 0
         except BaseException as e:  # noqa: BLE001 — surfaced after the call returns
             errors.append(e)
             return 1
 
-    def allreduce(_user, buf, n, _stream):
-        try:
-            if buf != scratch.data_ptr() or not 0 < n <= scratch.numel():
-                raise ValueError("nkv_arnoldi_dcgs2 allreduce callback: unexpected buffer")
-            ctx.comm.allreduce_(scratch[:n])
-            return 0
-        except BaseException as e:  # noqa: BLE001
-            errors.append(e)
-            return 1
-
     mv_c = _lib.MATVEC_FN(matvec)
-    ar_c = _lib.ALLREDUCE_FN(allreduce) if (ctx.comm.world > 1 or ctx.comm.force) else _lib.ALLREDUCE_FN()
+    ar_c = _allreduce_callback(ctx, scratch, errors)
     rc = lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(mstart), int(mend), Hd.t.data_ptr(), Hd.k + 1,
                                fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None, ar_c, None,
                                NKV_TIME_DOT if ctx.time_in_dot else 0, ctx.stream)

@@ -2001,6 +2001,38 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
     return nkv_normalize_dev(L, u, coef + 2 * m + 3, nullptr, 0, stream);
 }
 
+// update_hessenberg_matrix (krylov_decomposition.f90:103-189) as one call: the fused 3-pass CGS2
+// sequence of nekstab_next_amd/arnoldi.py (orthonormalize, mode "cgs2") with the all-reduce as a
+// callback — q_out = f/||f|| after two projections, H column in hcol_dev[0:j+1].
+int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
+                          double* hcol_dev, double* scratch_dev, void* ws, nkv_allreduce_fn allreduce, void* ar_user,
+                          unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    if (!hcol_dev || !scratch_dev) return fail(NKV_EINVAL, "hcol/scratch is NULL");
+    if (j < 0 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 0..%d", j, NKV_MAX_COLS);
+    const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+    double* h1 = scratch_dev;
+    double* h2 = scratch_dev + (j + 1);
+    double* nrm = scratch_dev + 2 * (j + 1);
+    auto reduce = [&](double* buf, int n, const char* what) -> int {
+        if (!allreduce) return NKV_OK;
+        const int rc = allreduce(ar_user, buf, n, stream);
+        return rc == 0 ? NKV_OK : fail(NKV_EINVAL, "allreduce callback returned %d (%s)", rc, what);
+    };
+    if (j == 0) {   // only normalise (the seed)
+        CHECK(nkv_dot(L, w, f, f, nrm, ws, tf, stream));
+        CHECK(reduce(nrm, 1, "norm"));
+        return nkv_arnoldi_finish(L, f, nrm, q_out, 0, h1, nullptr, hcol_dev, 0, stream);
+    }
+    CHECK(nkv_block_dot(L, w, Q, j, f, h1, ws, tf, stream));
+    CHECK(reduce(h1, j, "first projection"));
+    CHECK(nkv_block_update_dot(L, w, Q, j, h1, f, h2, ws, NKV_TIME | (tf ? NKV_TIME_DOT : 0u), stream));
+    CHECK(reduce(h2, j, "second projection"));
+    CHECK(nkv_block_update(L, w, Q, j, h2, f, nrm, ws, NKV_TIME | NKV_NORM2 | tf, stream));
+    CHECK(reduce(nrm, 1, "norm"));
+    return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
+}
+
 int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,
                        int j, const double* h1_dev, const double* h2_dev, double* hcol_dev,
                        unsigned flags, void* stream) {

@@ -266,7 +266,8 @@ def test_rotate_cols_row_bands(gpu, n_out):
 @pytest.mark.parametrize("name", list(LAYOUTS) + ["large"])
 def test_native_dcgs2_driver_bit_identical(gpu, name):
     """nkv_arnoldi_dcgs2 (the whole DCGS2 factorisation in one ABI call, operator as a callback)
-    gives the Python-driven DCGS2 factorisation bit for bit — from the seed and from mstart > 1."""
+    gives the Python-driven DCGS2 factorisation bit for bit — from the seed and from mstart > 1 —
+    and nkv_update_hessenberg (one call per CGS2 column) the Python-driven CGS2 one."""
     from nekstab_next_amd.layout import box3d_layout
 
     lay = box3d_layout(4000) if name == "large" else LAYOUTS[name]
@@ -275,7 +276,7 @@ def test_native_dcgs2_driver_bit_identical(gpu, name):
     op = DiagOperator(ctx, d)
     m = 20
     out = {}
-    for mode in ("dcgs2", "dcgs2-native"):
+    for mode in ("dcgs2", "dcgs2-native", "cgs2", "cgs2-native"):
         Q = ctx.basis(m + 1)
         Q[0].fill_hash(5)
         k_normalize(Q[0])
@@ -283,8 +284,9 @@ def test_native_dcgs2_driver_bit_identical(gpu, name):
         arnoldi_factorization(ctx, op, Q, Hd, 1, 12, mode=mode)
         arnoldi_factorization(ctx, op, Q, Hd, 13, m, mode=mode)   # continue from column 12 (mstart > 1)
         out[mode] = (Hd.download(), Q.storage.cpu().numpy())
-    np.testing.assert_array_equal(out["dcgs2"][0], out["dcgs2-native"][0])
-    np.testing.assert_array_equal(out["dcgs2"][1], out["dcgs2-native"][1])
+    for a, b in (("dcgs2", "dcgs2-native"), ("cgs2", "cgs2-native")):
+        np.testing.assert_array_equal(out[a][0], out[b][0])
+        np.testing.assert_array_equal(out[a][1], out[b][1])
 
 
 def test_native_dcgs2_driver_callback_errors(gpu):
@@ -314,7 +316,7 @@ def test_native_dcgs2_driver_callback_errors(gpu):
     assert rc == L_.NKV_EINVAL and "matvec" in L_.last_error()
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "mgs2", "dcgs2", "dcgs2-lazy"])
+@pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "cgs2-native", "mgs2", "dcgs2", "dcgs2-lazy"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     lay = LAYOUTS[name]

@@ -160,17 +160,18 @@ for forced in (False, True):
     d, _ = syn.laplacian_shift_invert(lay)
     seed = ctx.vector()
     seed.fill_hash(11)
-    for mode in ("dcgs2", "cgs2", "dcgs2-native"):
+    for mode in ("dcgs2", "cgs2", "dcgs2-native", "cgs2-native"):
         r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4, mode=mode))
         out[(forced, mode)] = (r.vals, r.H, r.mstart_history)
     assert comm.max_scalar(3.0, device=ctx.device) == 3.0
-for mode in ("dcgs2", "cgs2", "dcgs2-native"):
+for mode in ("dcgs2", "cgs2", "dcgs2-native", "cgs2-native"):
     a, b = out[(False, mode)], out[(True, mode)]
     np.testing.assert_array_equal(a[0], b[0]); np.testing.assert_array_equal(a[1], b[1]); assert a[2] == b[2]
 # the library-driven factorisation (all-reduce through the callback when forced) equals the Python-driven one
 for forced in (False, True):
-    a, b = out[(forced, "dcgs2")], out[(forced, "dcgs2-native")]
-    np.testing.assert_array_equal(a[0], b[0]); np.testing.assert_array_equal(a[1], b[1]); assert a[2] == b[2]
+    for m1, m2 in (("dcgs2", "dcgs2-native"), ("cgs2", "cgs2-native")):
+        a, b = out[(forced, m1)], out[(forced, m2)]
+        np.testing.assert_array_equal(a[0], b[0]); np.testing.assert_array_equal(a[1], b[1]); assert a[2] == b[2]
 dist.destroy_process_group()
 print("RCCL path ok")
 '''

@@ -196,11 +196,12 @@ def test_config3_full_size_hessenberg_vs_oracle(gpu):
         del Q
 
 
-@pytest.mark.parametrize("E", [1996, 22728])
-def test_config4_gmres_vs_oracle(gpu, E):
+@pytest.mark.parametrize("E,mode", [(1996, "cgs2"), (22728, "cgs2"), (1996, "cgs2-native")])
+def test_config4_gmres_vs_oracle(gpu, E, mode):
     """Config 4: Newton–Krylov inner GMRES on J = D - I, k_dim=200, tol=1e-9 on beta**2
     (1cyl.usr:14, 1cyl.par:18,23), on the cylinder mesh (E=1996, N=175,648) and at BASELINE's
-    cylinder-scaled size (E=22,728, N=2,000,064)."""
+    cylinder-scaled size (E=22,728, N=2,000,064); "cgs2-native" runs every Arnoldi column through
+    the one-call nkv_update_hessenberg."""
     lay = cylinder_layout(E)
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=210)
@@ -210,7 +211,7 @@ def test_config4_gmres_vs_oracle(gpu, E):
     rhs = ctx.vector()
     rhs.fill_hash(3)
     sol = ctx.vector()
-    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=200, maxiter=10, tol=1e-9))
+    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=200, maxiter=10, tol=1e-9, mode=mode))
     assert info.converged
 
     dref = syn.to_reference_order(lay, d)
