@@ -25,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400):
+def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400, mode="dcgs2"):
     rank, world = world_rank_pair
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -49,14 +49,14 @@ def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400):
         d, _ = syn.laplacian_shift_invert(lay)
         seed = ctx.vector()
         seed.fill_hash(11)
-        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4))
+        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4, mode=mode))
         res["lap"] = (r.vals, r.residual, r.mstart_history, r.schur_cnt, r.H)
         lay2 = cylinder_layout(E_cyl).shard(rank, world)
         ctx2 = NekContext(lay2, weights=syn.mass_weights(lay2), comm=comm, max_cols=48)
         c, s, dr, _ = syn.rot2_operator(lay2)
         seed2 = ctx2.vector()
         seed2.fill_hash(5)
-        r2 = krylov_schur(ctx2, Rot2Operator(ctx2, c, s, dr), seed2, KrylovSchurConfig(k_dim=24, schur_tgt=2))
+        r2 = krylov_schur(ctx2, Rot2Operator(ctx2, c, s, dr), seed2, KrylovSchurConfig(k_dim=24, schur_tgt=2, mode=mode))
         res["rot"] = (r2.vals, r2.residual, r2.mstart_history, r2.schur_cnt, r2.H)
         out[(world, rank)] = res
     finally:
@@ -64,21 +64,23 @@ def _run_ks(world_rank_pair, out, port, E_box=96, E_cyl=400):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,E_box,E_cyl", [(2, 96, 400), (3, 97, 401), (8, 101, 403)])
-def test_ranks_match_one_rank(gpu, world, E_box, E_cyl):
+@pytest.mark.parametrize("world,E_box,E_cyl,mode", [(2, 96, 400, "dcgs2"), (3, 97, 401, "dcgs2"), (8, 101, 403, "dcgs2"),
+                                                   (2, 96, 400, "dcgs2-native"), (3, 97, 401, "cgs2-native")])
+def test_ranks_match_one_rank(gpu, world, E_box, E_cyl, mode):
     """Krylov–Schur on `world` gloo ranks sharing the GPU (the sharded HIP path, one shard per
     process) reproduces the one-rank run; (3, 97, 401) gives ragged shards (32/32/33 and
     133/134/134 elements); (8, 101, 403) rehearses the 8-way split of the driver's 8-GPU run with
-    ragged shards (12/13 and 50/51 elements)."""
+    ragged shards (12/13 and 50/51 elements); the "-native" modes run the one-call library drivers,
+    whose all-reduce callback then goes through gloo between the processes."""
     mgr = mp.Manager()
     out = mgr.dict()
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_run_ks, args=((0, 1), out, _free_port(), E_box, E_cyl))
+    p = ctx.Process(target=_run_ks, args=((0, 1), out, _free_port(), E_box, E_cyl, mode))
     p.start()
     p.join()
     assert p.exitcode == 0
     port = _free_port()
-    procs = [ctx.Process(target=_run_ks, args=((r, world), out, port, E_box, E_cyl)) for r in range(world)]
+    procs = [ctx.Process(target=_run_ks, args=((r, world), out, port, E_box, E_cyl, mode)) for r in range(world)]
     for q in procs:
         q.start()
     for q in procs:
