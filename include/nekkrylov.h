@@ -67,6 +67,7 @@ extern "C" {
 #define NKV_EHIP 2   /* HIP runtime error (see nkv_last_error)        */
 #define NKV_ENAN 3   /* NaN detected in a reduction (k_dot :57 guard)  */
 #define NKV_ESHAPE 4 /* layout not padded/aligned as documented above  */
+#define NKV_ECALLBACK 5 /* a host callback (operator, all-reduce) of a one-call driver failed */
 
 /* Flags. */
 #define NKV_TIME 0x1u      /* include the `time` slot (dot: add p.time*q.time; BLAS-1: update it) */
@@ -201,7 +202,7 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
  *   allreduce(ar_user, buf, n, stream): in-place SUM of n device doubles over the ranks, ordered on
  *   `stream` (ncclAllReduce on it, or a stream sync + MPI_Allreduce); NULL on a single rank.
  *   flags: NKV_TIME_DOT includes the time products in the dots (uparam(1)==2.1, k_dot :52-54).
- *   A callback's non-zero return stops the factorisation with NKV_EINVAL (see nkv_last_error). */
+ *   A callback's non-zero return stops the factorisation with NKV_ECALLBACK (see nkv_last_error). */
 typedef int (*nkv_matvec_fn)(void* user, const double* x, double* y, void* stream);
 typedef int (*nkv_allreduce_fn)(void* user, double* buf, int n, void* stream);
 size_t nkv_arnoldi_scratch_doubles(int m);

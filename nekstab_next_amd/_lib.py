@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 NKV_TILE = 4096
 NKV_MAX_COLS = 1024   # most columns per multi-dot (include/nekkrylov.h)
 NKV_ROT_MAX_K = 576   # most input columns per basis rotation (restart, lazy-basis materialisation)
-NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE = 0, 1, 2, 3, 4
+NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE, NKV_ECALLBACK = 0, 1, 2, 3, 4, 5
 NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2
 NKV_OVERWRITE = 0x4

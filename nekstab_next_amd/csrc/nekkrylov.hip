@@ -1981,10 +1981,10 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
         const int m = j - 1;
         double* u = col(m);
         int rc = matvec(mv_user, u, f, stream);
-        if (rc != 0) return fail(NKV_EINVAL, "matvec callback returned %d at step %d", rc, j);
+        if (rc != 0) return fail(NKV_ECALLBACK, "matvec callback returned %d at step %d", rc, j);
         CHECK(nkv_block_dot2(L, w, Q, j, u, f, hd, ws, tf | NKV_X_IS_LAST, stream));
         if (allreduce && (rc = allreduce(ar_user, hd, 2 * j, stream)) != 0)
-            return fail(NKV_EINVAL, "allreduce callback returned %d at step %d", rc, j);
+            return fail(NKV_ECALLBACK, "allreduce callback returned %d at step %d", rc, j);
         CHECK(nkv_dcgs2_coef(m, hd, hd + j, j == mstart ? nullptr : hd + m, H_dev, ldh, coef, ws, stream));
         CHECK(nkv_dcgs2_update(L, w, Q, m, coef, u, f, col(j), nullptr, ws, NKV_TIME, stream));
     }
@@ -1994,7 +1994,7 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
     CHECK(nkv_block_dot(L, w, Q, m + 1, u, hd, ws, tf, stream));
     if (allreduce) {
         const int rc = allreduce(ar_user, hd, m + 1, stream);
-        if (rc != 0) return fail(NKV_EINVAL, "allreduce callback returned %d (closing step)", rc);
+        if (rc != 0) return fail(NKV_ECALLBACK, "allreduce callback returned %d (closing step)", rc);
     }
     CHECK(nkv_dcgs2_coef(m, hd, nullptr, hd + m, H_dev, ldh, coef, ws, stream));
     CHECK(nkv_block_update(L, w, Q, m, hd, u, nullptr, ws, NKV_TIME, stream));
@@ -2017,7 +2017,7 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
     auto reduce = [&](double* buf, int n, const char* what) -> int {
         if (!allreduce) return NKV_OK;
         const int rc = allreduce(ar_user, buf, n, stream);
-        return rc == 0 ? NKV_OK : fail(NKV_EINVAL, "allreduce callback returned %d (%s)", rc, what);
+        return rc == 0 ? NKV_OK : fail(NKV_ECALLBACK, "allreduce callback returned %d (%s)", rc, what);
     };
     if (j == 0) {   // only normalise (the seed)
         CHECK(nkv_dot(L, w, f, f, nrm, ws, tf, stream));

@@ -101,7 +101,7 @@ def test_header_constants_match_python():
 
     txt = open(os.path.join(ROOT, "include", "nekkrylov.h")).read()
     defs = {k: int(v, 0) for k, v in re.findall(r"#define (NKV_[A-Z0-9_]+)\s+(0x[0-9a-f]+|\d+)u?", txt)}
-    for name in ("NKV_TILE", "NKV_MAX_COLS", "NKV_ROT_MAX_K", "NKV_OK", "NKV_EINVAL", "NKV_EHIP", "NKV_ENAN", "NKV_ESHAPE",
+    for name in ("NKV_TILE", "NKV_MAX_COLS", "NKV_ROT_MAX_K", "NKV_OK", "NKV_EINVAL", "NKV_EHIP", "NKV_ENAN", "NKV_ESHAPE", "NKV_ECALLBACK",
                  "NKV_TIME", "NKV_ACCUMULATE", "NKV_OVERWRITE", "NKV_NORM2", "NKV_TIME_DOT", "NKV_X_IS_LAST"):
         assert defs[name] == getattr(_lib, name), name
 
