@@ -291,7 +291,7 @@ def test_native_dcgs2_driver_bit_identical(gpu, name):
 
 def test_native_dcgs2_driver_callback_errors(gpu):
     """A failing operator callback stops nkv_arnoldi_dcgs2 with the callback's exception (Python)
-    and NKV_EINVAL (C ABI); a NULL matvec is refused."""
+    and NKV_ECALLBACK (C ABI) after the first call; a NULL matvec is refused (NKV_EINVAL)."""
     from nekstab_next_amd import _lib as L_
 
     lay = LAYOUTS["2d"]
@@ -314,6 +314,17 @@ def test_native_dcgs2_driver_callback_errors(gpu):
                                    scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(), None, L_.ALLREDUCE_FN(),
                                    None, 0, ctx.stream)
     assert rc == L_.NKV_EINVAL and "matvec" in L_.last_error()
+    # a callback that reports failure: NKV_ECALLBACK, no further steps
+    calls = []
+
+    def bad(_user, x, y, _stream):
+        calls.append(x)
+        return 7
+
+    rc = ctx.lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, 1, 4, Hd.t.data_ptr(), 5, f.ptr,
+                                   scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(bad), None, L_.ALLREDUCE_FN(),
+                                   None, 0, ctx.stream)
+    assert rc == L_.NKV_ECALLBACK and "returned 7" in L_.last_error() and len(calls) == 1
 
 
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "cgs2-native", "mgs2", "dcgs2", "dcgs2-lazy"])
