@@ -54,12 +54,49 @@ class BoostConv:
         self.init = False
         self._dum = ctx.vector()
         self._r = torch.zeros(1, dtype=torch.float64, device=ctx.device)
+        self._dd_dev = torch.zeros(bst_snp * bst_snp, dtype=torch.float64, device=ctx.device)   # row-major
+        self._nrm_dev = torch.zeros(bst_snp, dtype=torch.float64, device=ctx.device)
+        self._cc_dev = torch.zeros(bst_snp, dtype=torch.float64, device=ctx.device)
 
     def _dot(self, a: NekVector, b: NekVector) -> float:
         return self.ctx.dot(a, b, time=False)
 
     def qr_dec(self) -> None:
-        """Single-pass MGS QR of Y into Q and dd, reference operation order (fixedp.f90:331-385)."""
+        """Single-pass MGS QR of Y into Q and dd, reference operation order (fixedp.f90:331-385).
+
+        The dots and the projections stay on the device (the scalars never visit the host: one
+        synchronisation per QR instead of one per dot); the reference's guard on a numerically
+        zero column (norm^2 < 1e-60: Q(j) = 0, dd(j,j) = 1) needs the host, so a QR that meets one
+        is redone in the host-scalar form below."""
+        if not self._qr_dec_device():
+            self._qr_dec_host()
+
+    def _qr_dec_device(self) -> bool:
+        ctx, n = self.ctx, self.n
+        w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+        D, nrm = self._dd_dev, self._nrm_dev
+        D.zero_()
+        dum = self._dum
+        for j in range(n):
+            dum.copy_from(self.Y[j], time=False)
+            for i in range(j):
+                r = D[i * n + j: i * n + j + 1]
+                ctx.call("nkv_dot", w, dum.ptr, self.Q[i].ptr, r.data_ptr(), ws, 0, st)
+                ctx.comm.allreduce_(r)
+                ctx.call("nkv_axpy_dev", dum.ptr, r.data_ptr(), -1.0, self.Q[i].ptr, 0, st)
+            ctx.call("nkv_dot", w, dum.ptr, dum.ptr, nrm[j:j + 1].data_ptr(), ws, 0, st)
+            ctx.comm.allreduce_(nrm[j:j + 1])
+            # dd(j,j) = sqrt(norm^2), Q(j) = dum / dd(j,j) (the reference's scal by the reciprocal)
+            ctx.call("nkv_normalize_dev", dum.ptr, nrm[j:j + 1].data_ptr(), D[j * n + j:].data_ptr(), 0, st)
+            self.Q[j].copy_from(dum, time=False)
+        if bool((nrm[1:] < 1e-60).any()):   # the only host synchronisation of the QR
+            return False
+        self.dd = D.view(n, n).cpu().numpy()
+        if np.isnan(self.dd).any():
+            ctx.check_nan()
+        return True
+
+    def _qr_dec_host(self) -> None:
         ctx, n = self.ctx, self.n
         dd = np.zeros((n, n))
         dum = self._dum
@@ -101,7 +138,14 @@ class BoostConv:
         self.Y[r].axpby(1.0, rb, -1.0)           # y_rot -= rb
         self.X[r].axpby(1.0, self.Y[r], -1.0)    # x_rot -= y_rot
         self.qr_dec()
-        cc = np.array([self._dot(rb, self.Q[j]) for j in range(self.n)])
+        ctx = self.ctx
+        for j in range(self.n):   # <rb, Q(j)>, one dot each as the reference; one host read for all
+            c = self._cc_dev[j:j + 1]
+            ctx.call("nkv_dot", ctx.w.data_ptr(), rb.ptr, self.Q[j].ptr, c.data_ptr(), ctx.ws.data_ptr(), 0, ctx.stream)
+            ctx.comm.allreduce_(c)
+        cc = self._cc_dev.cpu().numpy()
+        if np.isnan(cc).any():
+            ctx.check_nan()
         ccb = linear_system(self.dd, cc)
         self.rot = (r + 1) % self.n
         self.Y[self.rot].copy_from(rb, time=False)

@@ -83,3 +83,30 @@ def test_boostconv_device_matches_oracle(gpu):
         got = unpad(v.to_packed())
         assert np.max(np.abs(got - ref[it])) <= 1e-9 * max(1.0, np.max(np.abs(ref[it]))), it
     assert np.max(np.abs(unpad(v.to_packed()) - vstar)) < 1e-6
+
+
+def test_boostconv_qr_device_equals_host_and_guard(gpu):
+    """The device-resident MGS QR (one host synchronisation) gives the host-scalar QR's dd and Q,
+    and a numerically zero column (the reference's guard, fixedp.f90:371-376: Q(j) = 0,
+    dd(j,j) = 1) sends the QR to the host form."""
+    from nekstab_next_amd.boostconv import BoostConv, velocity_layout
+    from nekstab_next_amd.vector import NekContext
+
+    lay = velocity_layout(NekLayout(ldim=2, lx1=4, lx2=2, nelgv=30))
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), max_cols=16)
+    n = 6
+    bc = BoostConv(ctx, n)
+    for j in range(n):
+        bc.Y[j].fill_hash(900 + j)
+    assert bc._qr_dec_device()
+    dd_dev, Q_dev = bc.dd.copy(), bc.Q.storage.cpu().numpy().copy()
+    bc._qr_dec_host()
+    np.testing.assert_allclose(dd_dev, bc.dd, rtol=1e-14, atol=1e-15)
+    np.testing.assert_allclose(Q_dev, bc.Q.storage.cpu().numpy(), rtol=0, atol=1e-14)
+    bc.Y[3].zero()   # a zero column: the guard
+    assert not bc._qr_dec_device()
+    bc.qr_dec()
+    assert bc.dd[3, 3] == 1.0 and not np.any(bc.Q[3].to_packed())
+    G = np.array([[ctx.dot(bc.Q[a], bc.Q[b], time=False) for b in range(n)] for a in range(n)])
+    keep = [0, 1, 2, 4, 5]
+    np.testing.assert_allclose(G[np.ix_(keep, keep)], np.eye(5), atol=1e-13)

@@ -9,7 +9,7 @@
 * f2 checkpoint: one KRY field file (Nek5000 #std, fp64) of an N=50,007,232 vector written and read
   back through the product's writer/reader (host I/O, device<->host copies included) — MB/s.
 * f4 BoostConv ``core`` (bst_snp = 10, velocity-only layout of the scaled cylinder, N=1,636,416 per
-  vector) — ms per call (its QR is the reference's MGS order with one host-synchronised dot each).
+  vector) — ms per call (its QR is the reference's MGS order, scalars device-resident).
 * f3 .fld I/O is host-only; its throughput is the f2 line.
 Prints one JSON object per measurement.
 """
@@ -121,8 +121,8 @@ def main():
     torch.cuda.synchronize()
     per = (time.perf_counter() - t0) / 3
     print(json.dumps(dict(row="f4_boostconv_core", N=vlay.N, bst_snp=10, ms_per_call=round(per * 1e3, 3),
-                          note="QR in the reference's MGS order, one host-synchronised dot per projection "
-                               "(fixedp.f90:331-385)")), flush=True)
+                          note="QR in the reference's MGS order (fixedp.f90:331-385), dots and projections "
+                               "device-resident: one host synchronisation per QR")), flush=True)
 
 
 if __name__ == "__main__":
