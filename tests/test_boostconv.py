@@ -85,6 +85,7 @@ def test_boostconv_device_matches_oracle(gpu):
     assert np.max(np.abs(unpad(v.to_packed()) - vstar)) < 1e-6
 
 
+@pytest.mark.gpu
 def test_boostconv_qr_device_equals_host_and_guard(gpu):
     """The device-resident MGS QR (one host synchronisation) gives the host-scalar QR's dd and Q,
     and a numerically zero column (the reference's guard, fixedp.f90:371-376: Q(j) = 0,
