@@ -46,6 +46,15 @@ namespace {
 #ifndef NKV_FUSE_G
 #define NKV_FUSE_G 1024  // workgroups of the fused update+dot
 #endif
+#ifndef NKV_FUSE_G_MID
+#define NKV_FUSE_G_MID 512  // ... for NKV_FUSE_MID_LO <= j <= NKV_FUSE_MID_HI: +5-8 % at N = 1.25e7,
+#endif                      // 5e7 and 1e8 (profiles/r02ao_tune_fmid.log)
+#ifndef NKV_FUSE_MID_LO
+#define NKV_FUSE_MID_LO 16
+#endif
+#ifndef NKV_FUSE_MID_HI
+#define NKV_FUSE_MID_HI 32
+#endif
 #ifndef NKV_DC_PAIRS
 #define NKV_DC_PAIRS 8  // double2 per thread per tile in the DCGS2 kernels (large problems)
 #endif
@@ -1749,7 +1758,10 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     const int64_t tiles_total = rows / kFuseRows;
     const int64_t tpf = L->sv / kFuseRows;
     const int64_t tiles_w = tpf * L->n_wf;
-    int64_t g = tiles_total < NKV_FUSE_G ? tiles_total : NKV_FUSE_G;
+    // mid-size column counts run the fused pass on a smaller grid (NKV_FUSE_G_MID workgroups for
+    // NKV_FUSE_MID_LO <= j <= NKV_FUSE_MID_HI)
+    const int64_t gcap = (j >= NKV_FUSE_MID_LO && j <= NKV_FUSE_MID_HI) ? NKV_FUSE_G_MID : NKV_FUSE_G;
+    int64_t g = tiles_total < gcap ? tiles_total : gcap;
     if (g < 1) g = 1;
     const int B = (int)g;
     const int64_t T = rows;

@@ -96,6 +96,9 @@ VARIANTS = {
     "x_bu_g1024_r1": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 1},
     "x_bu_g1024_r2": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 2},
     "x_rs_b128": {"src": "exp", "NKVX_ROTS_B128": 1},
+    "fmid512": {"NKV_FUSE_G_MID": 512},
+    "fmid384": {"NKV_FUSE_G_MID": 384},
+    "fmid768": {"NKV_FUSE_G_MID": 768},
     "ps4": {"NKV_PAIRS_SMALL": 4},
     "ps1": {"NKV_PAIRS_SMALL": 1},
     "d2u4": {"NKV_D2_U": 4},
