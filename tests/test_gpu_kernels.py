@@ -325,6 +325,17 @@ def test_native_dcgs2_driver_callback_errors(gpu):
                                    scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(bad), None, L_.ALLREDUCE_FN(),
                                    None, 0, ctx.stream)
     assert rc == L_.NKV_ECALLBACK and "returned 7" in L_.last_error() and len(calls) == 1
+    # argument checks (no launch): ldh too small, mstart 0, scratch NULL; nkv_update_hessenberg j < 0
+    good = L_.MATVEC_FN(lambda *_: 0)
+    for args, what in (((1, 4, 4, scratch.data_ptr()), "ldh"), ((0, 4, 5, scratch.data_ptr()), "outside"),
+                       ((1, 4, 5, None), "scratch")):
+        ms, me, ldh, scr = args
+        rc = ctx.lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, ms, me, Hd.t.data_ptr(), ldh, f.ptr, scr,
+                                       ctx.ws.data_ptr(), good, None, L_.ALLREDUCE_FN(), None, 0, ctx.stream)
+        assert rc == L_.NKV_EINVAL and what in L_.last_error(), (args, L_.last_error())
+    rc = ctx.lib.nkv_update_hessenberg(ctx._Lp, ctx.w.data_ptr(), Q.ptr, -1, f.ptr, Q.col_ptr(1), Hd.t.data_ptr(),
+                                       scratch.data_ptr(), ctx.ws.data_ptr(), L_.ALLREDUCE_FN(), None, 0, ctx.stream)
+    assert rc == L_.NKV_EINVAL
 
 
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "cgs2-native", "mgs2", "dcgs2", "dcgs2-lazy"])
