@@ -197,7 +197,8 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
  *   factorisation so far (row mstart-1 the restart row).  On return Q columns 0..mend and H columns
  *   0..mend-1 form an Arnoldi factorisation A Q_mend = Q_{mend+1} H.
  *   H_dev: device, column-major, leading dimension ldh >= mend+1.  f: one device vector (scratch).
- *   scratch_dev: nkv_arnoldi_scratch_doubles(mend) doubles of device memory; ws as for the dots.
+ *   scratch_dev: nkv_arnoldi_scratch_doubles(mend) doubles of device memory; ws: at least
+ *   nkv_workspace_bytes(L, mend + 1) bytes (the multi-dots' partials for up to mend+1 columns).
  *   matvec(mv_user, x, y, stream): y = A x for device vectors x, y, enqueued on `stream`; returns 0.
  *   allreduce(ar_user, buf, n, stream): in-place SUM of n device doubles over the ranks, ordered on
  *   `stream` (ncclAllReduce on it, or a stream sync + MPI_Allreduce); NULL on a single rank.
@@ -215,7 +216,8 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
  * block_update_dot, all-reduce, block_update + norm, all-reduce, arnoldi_finish) with the
  * all-reduce as the callback of nkv_arnoldi_dcgs2 (NULL on one rank).  f is orthogonalised twice
  * against Q[:,0:j] (W inner product), q_out = f/||f||_W, hcol_dev[0:j+1] = H(1:k+1, k).  j = 0
- * only normalises.  scratch_dev: nkv_arnoldi_scratch_doubles(j) doubles.  flags: NKV_TIME_DOT
+ * only normalises.  scratch_dev: nkv_arnoldi_scratch_doubles(j) doubles; ws: nkv_workspace_bytes(L, j)
+ * bytes at least.  flags: NKV_TIME_DOT
  * (time products in the dots).  For per-column consumers (GMRES: newton_krylov.f90:252) and
  * checkpointing Arnoldi, where each column must be final when its step returns. */
 int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
