@@ -20,6 +20,8 @@ class KrylovSchurConfig:
     lazy_basis: bool = False       # dcgs2: leave finished columns as Q = S T (one vector write less per
     #                                step; the restart folds T in, the result basis is materialised once;
     #                                measured +0.3 % at N=1e8, m=128 -- DESIGN.md §6)
+    breakdown_tol: float = 1e-8    # |H(c+1,c)| < tol * ||H(1:c+2,c)||: the Krylov space became invariant;
+    #                                that factorisation is redone in the reference's MGS2 order
 
 
 @dataclass

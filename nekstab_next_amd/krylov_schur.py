@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from . import lapack
+from ._lib import NkvNaNError
 from .arnoldi import FactorizationGraph, HessenbergDev, arnoldi_factorization
 from .config import KrylovSchurConfig
 from .operators import LinearOperator
@@ -45,6 +46,25 @@ class KrylovSchurResult:
     mstart_history: list = field(default_factory=list)   # mstart after each condensation
     cnt_history: list = field(default_factory=list)      # converged count after each factorisation
     selected_history: list = field(default_factory=list)  # selected masks per condensation
+    breakdowns: list = field(default_factory=list)        # mstart of each factorisation redone in MGS2
+
+
+def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float) -> int:
+    """First Arnoldi column c in [c0, k) whose new direction vanished (|H(c+1,c)| < tol ||H(0:c+2,c)||,
+    the Krylov space is invariant to rounding), or that holds a non-finite entry; -1 if none.
+
+    At such a step the reference's MGS2 (eigensolvers.f90:101-112) still produces a unit vector from the
+    rounding noise, orthogonalised twice one projection at a time.  The one-pass classical forms cannot:
+    CGS2 leaves O(eps/ratio) components in span(Q) (garbage at ratio ~ eps), and DCGS2's Pythagorean
+    norm sqrt(||u||^2 - ||Q^T u||^2) cancels to a negative (NaN).  Normal runs sit at ratios >= 0.1."""
+    for c in range(max(c0, 0), k):
+        col = H[:c + 2, c]
+        if not np.all(np.isfinite(col)):
+            return c
+        nrm = float(np.linalg.norm(col))
+        if nrm == 0.0 or abs(col[c + 1]) < tol * nrm:
+            return c
+    return -1
 
 
 def prepare_seed(seed: NekVector, Q0: NekVector) -> float:
@@ -144,14 +164,43 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     mode = "mgs2" if (cfg.seed_mode == "noise" and start is None) else cfg.mode
     if mode != cfg.mode:
         graphs, lazy = None, False
+    snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)
     while True:
-        if graphs is not None:
-            graphs.run(mstart, k, transpose)
-        else:
-            arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose, on_step=hook,
-                                  lazy=lazy)
-        H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
-        ctx.check_nan()
+        if mode != "mgs2":
+            H_before = H.copy()
+            snap = snap if snap is not None else ctx.vector()
+            snap.storage.copy_(Q.storage[mstart - 1])
+        broken = False
+        try:
+            if graphs is not None:
+                graphs.run(mstart, k, transpose)
+            else:
+                arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose,
+                                      on_step=hook, lazy=lazy)
+            H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
+            ctx.check_nan()
+        except NkvNaNError:
+            if mode == "mgs2":
+                raise
+            broken = True
+        if mode != "mgs2":
+            broken = broken or breakdown_column(H, mstart - 1, k, cfg.breakdown_tol) >= 0
+            if ctx.comm.world > 1:   # the H test is replicated; the NaN flag is per rank
+                flag = torch.tensor([1.0 if broken else 0.0], dtype=torch.float64, device=ctx.device)
+                broken = float(ctx.comm.allreduce_(flag).item()) > 0.0
+            if broken:
+                # invariant subspace reached: redo this factorisation from its starting state in the
+                # reference's MGS2 order, and keep that order for the rest of the solve
+                res.breakdowns.append(mstart)
+                Q.reset_T()   # a lazy factorisation leaves Q = S T from Q(mstart) on; T was I before
+                Q.storage[mstart - 1].copy_(snap.storage)
+                H[...] = H_before
+                Hd.upload(H)
+                mode, graphs, lazy = "mgs2", None, False
+                arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose,
+                                      on_step=hook)
+                H[...] = Hd.download()
+                ctx.check_nan()
         vals, vecs = lapack.eig(H[:k, :k])
         residual = np.abs(H[k, k - 1] * vecs[k - 1, :])
         cnt = int(np.count_nonzero(residual < cfg.eigen_tol))

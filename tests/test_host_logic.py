@@ -136,3 +136,22 @@ def test_sort_eigendecomp_python_equals_c(n):
         v2, e2 = orc.sort_eigendecomp(vals.copy(), vecs.copy())
         np.testing.assert_array_equal(v1, v2)
         np.testing.assert_array_equal(e1, e2)
+
+
+def test_breakdown_column_rule():
+    """Invariant-subspace detection on the host H (krylov_schur.breakdown_column): the first Arnoldi
+    column from ``c0`` whose subdiagonal is below tol x its column norm, or that is non-finite."""
+    from nekstab_next_amd.krylov_schur import breakdown_column
+
+    k = 6
+    H = np.triu(np.ones((k + 1, k)), -1)
+    assert breakdown_column(H, 0, k, 1e-8) == -1
+    H[4, 3] = 1e-12
+    assert breakdown_column(H, 0, k, 1e-8) == 3
+    assert breakdown_column(H, 4, k, 1e-8) == -1      # columns before c0 are the restart block
+    assert breakdown_column(H, 0, k, 1e-13) == -1
+    H[2, 1] = np.nan
+    assert breakdown_column(H, 0, k, 1e-8) == 1
+    H[2, 1] = 1.0
+    H[:, 5] = 0.0
+    assert breakdown_column(H, 4, k, 1e-8) == 5
