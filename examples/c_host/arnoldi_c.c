@@ -11,7 +11,10 @@
  * identity), the closing re-orthogonalisation, then checks of W-orthonormality of the basis and of
  * the Arnoldi relation A Q_m = Q_{m+1} H through the same ABI; then the same factorisation as ONE
  * call of the native driver nkv_arnoldi_dcgs2 (the operator as a callback), which must reproduce
- * Q and H bit for bit.  Exit status 0 on success.
+ * Q and H bit for bit.  Last, the breakdown protocol of include/nekkrylov.h on a rank-3 operator:
+ * nkv_arnoldi_dcgs2 with NKV_CHECK_BREAKDOWN returns NKV_EBREAKDOWN, the host restores the seed
+ * column and redoes the factorisation with nkv_arnoldi_factorization(NKV_MGS2) (the reference's
+ * order), whose basis must be W-orthonormal.  Exit status 0 on success.
  */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -175,7 +178,34 @@ int main(int argc, char** argv) {
     }
     printf("arnoldi_c: nkv_arnoldi_dcgs2 (one call) %s the step-by-step loop\n",
            same ? "equals bit for bit" : "DIFFERS from");
-    const int ok = orth < 1e-12 && arn / hmax < 1e-12 && same;
+
+    /* breakdown: d = diag(0.95, 0.85, 0.75) on three points, 0 elsewhere (the Krylov space of the
+       seed closes after 4 steps: the seed and the three eigen-directions).  DCGS2 with the check -> NKV_EBREAKDOWN; restore and redo in MGS2 order. */
+    for (int64_t i = 0; i < L.ld; ++i) hdg[i] = 0.0;
+    hdg[7] = 0.95, hdg[14] = 0.85, hdg[21] = 0.75;
+    HK(hipMemcpyAsync(d, hdg, vbytes, hipMemcpyHostToDevice, st));
+    HK(hipMemcpyAsync(Q2, Q, vbytes, hipMemcpyDeviceToDevice, st));   /* the normalised seed */
+    HK(hipMemsetAsync(Hd2, 0, (size_t)m * (m + 1) * sizeof(double), st));
+    const int rb = nkv_arnoldi_dcgs2(&L, w, Q2, 1, m, Hd2, m + 1, f, scr, ws, diag_matvec, &op, NULL, NULL,
+                                     NKV_CHECK_BREAKDOWN, st);
+    printf("arnoldi_c: rank-3 operator, nkv_arnoldi_dcgs2 + NKV_CHECK_BREAKDOWN -> %d (%s)\n", rb,
+           rb == NKV_OK ? "" : nkv_last_error());
+    HK(hipMemcpyAsync(Q2, Q, vbytes, hipMemcpyDeviceToDevice, st));   /* restore Q(mstart) and H */
+    HK(hipMemsetAsync(Hd2, 0, (size_t)m * (m + 1) * sizeof(double), st));
+    CK(nkv_arnoldi_factorization(&L, w, Q2, 1, m, Hd2, m + 1, f, scr, ws, diag_matvec, &op, NULL, NULL, NKV_MGS2, st));
+    CK(nkv_check_status(ws, st));
+    double orth2 = 0.0;
+    for (int c = 0; c <= m; ++c) {
+        CK(nkv_block_dot(&L, w, Q2, m + 1, Q2 + (int64_t)c * L.ld, hd, ws, 0, st));
+        HK(hipMemcpyAsync(g, hd, (size_t)(m + 1) * sizeof(double), hipMemcpyDeviceToHost, st));
+        HK(hipStreamSynchronize(st));
+        for (int r = 0; r <= m; ++r) orth2 = fmax(orth2, fabs(g[r] - (r == c ? 1.0 : 0.0)));
+    }
+    HK(hipMemcpy(H2, Hd2, (size_t)m * (m + 1) * sizeof(double), hipMemcpyDeviceToHost));
+    printf("arnoldi_c: MGS2 fallback: H(5,4) = %.3e (span{q1, A q1, ...} invariant after 4 steps), max|Q^T W Q - I| = %.3e\n",
+           H2[3 * (m + 1) + 4], orth2);
+    const int ok = orth < 1e-12 && arn / hmax < 1e-12 && same && rb == NKV_EBREAKDOWN && orth2 < 1e-8 &&
+                   fabs(H2[3 * (m + 1) + 4]) < 1e-12;
     printf(ok ? "arnoldi_c: OK\n" : "arnoldi_c: FAILED\n");
     (void)rows;
     return ok ? 0 : 1;

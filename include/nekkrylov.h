@@ -68,6 +68,7 @@ extern "C" {
 #define NKV_ENAN 3   /* NaN detected in a reduction (k_dot :57 guard)  */
 #define NKV_ESHAPE 4 /* layout not padded/aligned as documented above  */
 #define NKV_ECALLBACK 5 /* a host callback (operator, all-reduce) of a one-call driver failed */
+#define NKV_EBREAKDOWN 6 /* NKV_CHECK_BREAKDOWN: the Krylov space became invariant (nkv_arnoldi_factorization) */
 
 /* Flags. */
 #define NKV_TIME 0x1u      /* include the `time` slot (dot: add p.time*q.time; BLAS-1: update it) */
@@ -76,6 +77,8 @@ extern "C" {
 #define NKV_NORM2 0x8u      /* block_update: also write the local ||f||_W^2 partial               */
 #define NKV_TIME_DOT 0x10u  /* block_update_dot: include the time product in the dot partial      */
 #define NKV_X_IS_LAST 0x20u /* block_dot2: x is column j-1 of Q (its two dots come from registers)  */
+#define NKV_MGS2 0x40u      /* update_hessenberg / arnoldi_factorization: the reference's MGS2 order */
+#define NKV_CHECK_BREAKDOWN 0x80u /* one-call factorisations: check the new H columns on return      */
 
 typedef struct nkv_layout {
     int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */
@@ -202,7 +205,8 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
  *   matvec(mv_user, x, y, stream): y = A x for device vectors x, y, enqueued on `stream`; returns 0.
  *   allreduce(ar_user, buf, n, stream): in-place SUM of n device doubles over the ranks, ordered on
  *   `stream` (ncclAllReduce on it, or a stream sync + MPI_Allreduce); NULL on a single rank.
- *   flags: NKV_TIME_DOT includes the time products in the dots (uparam(1)==2.1, k_dot :52-54).
+ *   flags: NKV_TIME_DOT includes the time products in the dots (uparam(1)==2.1, k_dot :52-54);
+ *   NKV_CHECK_BREAKDOWN: see "Breakdown" under nkv_arnoldi_factorization below.
  *   A callback's non-zero return stops the factorisation with NKV_ECALLBACK (see nkv_last_error). */
 typedef int (*nkv_matvec_fn)(void* user, const double* x, double* y, void* stream);
 typedef int (*nkv_allreduce_fn)(void* user, double* buf, int n, void* stream);
@@ -218,11 +222,34 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
  * against Q[:,0:j] (W inner product), q_out = f/||f||_W, hcol_dev[0:j+1] = H(1:k+1, k).  j = 0
  * only normalises.  scratch_dev: nkv_arnoldi_scratch_doubles(j) doubles; ws: nkv_workspace_bytes(L, j)
  * bytes at least.  flags: NKV_TIME_DOT
- * (time products in the dots).  For per-column consumers (GMRES: newton_krylov.f90:252) and
+ * (time products in the dots); NKV_MGS2: the reference's own order instead (:155-186, two MGS passes,
+ * one dot + all-reduce + axpy per column; j+3 scratch doubles).  For per-column consumers (GMRES: newton_krylov.f90:252) and
  * checkpointing Arnoldi, where each column must be final when its step returns. */
 int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
                           double* hcol_dev, double* scratch_dev, void* ws, nkv_allreduce_fn allreduce, void* ar_user,
                           unsigned flags, void* stream);
+
+/* arnoldi_factorization (krylov_decomposition.f90:2-99) with per-column orthogonalisation: for
+ * mstep = mstart..mend, matvec(Q col mstep-1 -> f), then nkv_update_hessenberg(Q, mstep, f,
+ * q_out = Q col mstep, hcol = H col mstep-1).  Same arguments as nkv_arnoldi_dcgs2; every column is
+ * final when its step ends and columns < mstart are never written.  flags: NKV_TIME_DOT,
+ * NKV_MGS2 (the reference's operation order, its dots all-reduced one at a time through the
+ * callback: the sharded form of nkv_mgs2_step), NKV_CHECK_BREAKDOWN.
+ *
+ * Breakdown (both one-call factorisations).  When the operator's Krylov space closes before mend
+ * (A restricted to span(Q) is invariant: a rank-deficient operator), each later f is rounding noise.
+ * The reference's MGS2 normalises the noise and carries on; the classical forms cannot: DCGS2's
+ * norm sqrt(||u||^2 - ||Q^T W u||^2) cancels to a negative (NaN) and CGS2 leaves O(eps/ratio)
+ * components in span(Q).  With NKV_CHECK_BREAKDOWN the driver synchronises the stream on return,
+ * and returns NKV_EBREAKDOWN (message: the column and its ratio) if the NaN flag is set (it is
+ * cleared) or any new column c has a non-finite entry or |H(c+1,c)| < 1e-8 ||H(0:c+2,c)||.  Normal
+ * runs sit at ratios >= 0.1.  nkv_arnoldi_dcgs2 has by then rewritten Q column mstart-1 and H row
+ * mstart-1 (the delayed re-orthogonalisation of the seed column): the caller restores both from its
+ * own copies and redoes the factorisation with nkv_arnoldi_factorization(..., NKV_MGS2, ...), as
+ * nekstab_next_amd.krylov_schur does. */
+int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
+                              int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
+                              void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
 
 /* DCGS2 over a LAZY basis (same replacement target): the finished q_j is never written.  The stored
  * columns S_0..S_{m-1} keep the raw provisional vectors and the orthonormal basis is Q = S T with

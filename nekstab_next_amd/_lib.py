@@ -20,13 +20,15 @@ LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 NKV_TILE = 4096
 NKV_MAX_COLS = 1024   # most columns per multi-dot (include/nekkrylov.h)
 NKV_ROT_MAX_K = 576   # most input columns per basis rotation (restart, lazy-basis materialisation)
-NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE, NKV_ECALLBACK = 0, 1, 2, 3, 4, 5
+NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE, NKV_ECALLBACK, NKV_EBREAKDOWN = 0, 1, 2, 3, 4, 5, 6
 NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2
 NKV_OVERWRITE = 0x4
 NKV_NORM2 = 0x8
 NKV_TIME_DOT = 0x10
 NKV_X_IS_LAST = 0x20
+NKV_MGS2 = 0x40
+NKV_CHECK_BREAKDOWN = 0x80
 
 
 class NkvError(RuntimeError):
@@ -39,6 +41,10 @@ class NkvError(RuntimeError):
 
 class NkvNaNError(NkvError, FloatingPointError):
     """NaN detected in a dot product (reference aborts: core/nek_vectors.f90:108-111)."""
+
+
+class NkvBreakdownError(NkvError):
+    """NKV_CHECK_BREAKDOWN: a one-call factorisation reached an invariant subspace (include/nekkrylov.h)."""
 
 
 class nkv_layout(Structure):
@@ -85,6 +91,8 @@ _SIGNATURES = {
     "nkv_arnoldi_dcgs2": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P, ALLREDUCE_FN, _P,
                                   c_uint, _P]),
     "nkv_update_hessenberg": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, _P, ALLREDUCE_FN, _P, c_uint, _P]),
+    "nkv_arnoldi_factorization": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P,
+                                          ALLREDUCE_FN, _P, c_uint, _P]),
     "nkv_combine": (c_int, [_L, _P, c_int, _P, _P, c_uint, _P]),
     "nkv_normalize_store": (c_int, [_L, _P, _P, _P, _P, c_uint, _P]),
     "nkv_mgs2_step": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
@@ -136,6 +144,8 @@ def check(code: int, where: str) -> None:
     msg = last_error()
     if code == NKV_ENAN:
         raise NkvNaNError(code, where, msg)
+    if code == NKV_EBREAKDOWN:
+        raise NkvBreakdownError(code, where, msg)
     raise NkvError(code, where, msg)
 
 

@@ -82,12 +82,13 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
     projection coefficients h1+h2 go to hcol[0:j] and ||f|| to hcol[j] (device memory).  j = 0
     only normalises."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
-    if mode == "cgs2-native":   # the same CGS2 sequence as ONE library call (nkv_update_hessenberg)
+    if mode in ("cgs2-native", "mgs2-native"):   # the cgs2 / mgs2 sequence as ONE library call
         scratch = _native_scratch(ctx, j)
         errors = []
         ar_c = _allreduce_callback(ctx, scratch, errors)
+        flags = (NKV_TIME_DOT if ctx.time_in_dot else 0) | (_lib.NKV_MGS2 if mode == "mgs2-native" else 0)
         rc = ctx.lib.nkv_update_hessenberg(ctx._Lp, w, Q.ptr, int(j), f.ptr, out_ptr, hcol_ptr, scratch.data_ptr(), ws,
-                                           ar_c, None, NKV_TIME_DOT if ctx.time_in_dot else 0, st)
+                                           ar_c, None, flags, st)
         if errors:
             raise errors[0]
         _lib.check(rc, "nkv_update_hessenberg")
@@ -288,11 +289,13 @@ def _allreduce_callback(ctx: NekContext, scratch: torch.Tensor, errors: list):
 
 
 def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int, mend: int,
-                  f: NekVector, transpose: bool) -> None:
+                  f: NekVector, transpose: bool, entry: str = "nkv_arnoldi_dcgs2", flags: int = 0) -> None:
     """The DCGS2 factorisation as ONE library call (``nkv_arnoldi_dcgs2``, include/nekkrylov.h): the
     C++ side runs the step sequence of ``_dcgs2_step`` / ``_dcgs2_close`` (same entry points, same
     order, so the result is bit-identical to ``mode="dcgs2"``) and calls back for the operator and
-    the all-reduce — the shape a Fortran host uses to replace ``arnoldi_factorization``."""
+    the all-reduce — the shape a Fortran host uses to replace ``arnoldi_factorization``.
+    ``entry="nkv_arnoldi_factorization"``: the per-column cgs2 (or, with ``NKV_MGS2`` in ``flags``,
+    mgs2) factorisation as one call, bit-identical to those modes."""
     lib = ctx.lib
     scratch = _native_scratch(ctx, mend)
     base, ld8, fptr = Q.ptr, 8 * ctx.layout.ld, f.ptr
@@ -303,7 +306,7 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
         try:
             c, r = divmod((x or 0) - base, ld8)
             if r or not 0 <= c < Q.k or y != fptr:
-                raise ValueError(f"nkv_arnoldi_dcgs2 matvec callback: x={x}, y={y} are not a basis column and f")
+                raise ValueError(f"{entry} matvec callback: x={x}, y={y} are not a basis column and f")
             apply(Q[c], f)
             return 0
         except BaseException as e:  # noqa: BLE001 — surfaced after the call returns
@@ -312,12 +315,12 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
 
     mv_c = _lib.MATVEC_FN(matvec)
     ar_c = _allreduce_callback(ctx, scratch, errors)
-    rc = lib.nkv_arnoldi_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(mstart), int(mend), Hd.t.data_ptr(), Hd.k + 1,
-                               fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None, ar_c, None,
-                               NKV_TIME_DOT if ctx.time_in_dot else 0, ctx.stream)
+    rc = getattr(lib, entry)(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(mstart), int(mend), Hd.t.data_ptr(), Hd.k + 1,
+                             fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None, ar_c, None,
+                             (NKV_TIME_DOT if ctx.time_in_dot else 0) | flags, ctx.stream)
     if errors:
         raise errors[0]
-    _lib.check(rc, "nkv_arnoldi_dcgs2")
+    _lib.check(rc, entry)
 
 
 def _settle_basis(Q: Basis, mstart: int, lazy: bool) -> None:
@@ -358,6 +361,13 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
             _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose)
             return
         mode = "dcgs2"
+    if mode in ("cgs2-native", "mgs2-native") and on_step is None:   # per-column modes, one ABI call
+        if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+            raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        _settle_basis(Q, mstart, lazy=False)
+        _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
+                      flags=_lib.NKV_MGS2 if mode == "mgs2-native" else 0)
+        return
     if mode == "dcgs2" and on_step is None:
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")

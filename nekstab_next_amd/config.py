@@ -12,7 +12,9 @@ class KrylovSchurConfig:
     schur_del: float = 0.1    # keep |lambda| >= 1 - schur_del at restarts (:12)
     maxmodes: int = 20        # max eigenmodes exported (:13)
     mode: str = "dcgs2"       # "dcgs2" (block CGS2, delayed re-orth.: 2 reads of Q per step, the MI355X
-    #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order)
+    #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order);
+    #                           "dcgs2-native" | "cgs2-native" | "mgs2-native": the same sequences driven
+    #                           by the library's one-call entry points (bit-identical)
     seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "as_is"
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it

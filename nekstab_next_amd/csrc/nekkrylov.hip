@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "nekkrylov.h"
@@ -1974,6 +1975,46 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
 // without Python: the caller supplies the operator and the all-reduce as callbacks.
 size_t nkv_arnoldi_scratch_doubles(int m) { return (size_t)(2 * (m + 1) + 4 * m + 16); }
 
+// NKV_CHECK_BREAKDOWN: after a one-call factorisation, synchronise and test the new H columns c0..c1-1
+// (include/nekkrylov.h, "Breakdown").  The same rule as nekstab_next_amd.krylov_schur.breakdown_column.
+static constexpr double kBreakdownTol = 1e-8;
+
+static int check_breakdown(const double* H_dev, int64_t ldh, int c0, int c1, void* ws, void* stream) {
+    if (c0 < 0) c0 = 0;
+    if (c1 <= c0) return NKV_OK;
+    hipStream_t st = S(stream);
+    const size_t n = (size_t)ldh * (size_t)(c1 - c0);
+    double* h = static_cast<double*>(malloc(n * sizeof(double)));
+    if (!h) return fail(NKV_EINVAL, "breakdown check: host allocation of %zu doubles failed", n);
+    int flag = 0;
+    hipError_t e = hipMemcpyAsync(h, H_dev + (int64_t)c0 * ldh, n * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&flag, nan_flag_of(ws), sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(NKV_EHIP, "breakdown check: %s", hipGetErrorString(e));
+    }
+    int bad = -1;
+    double ratio = 0.0;
+    for (int c = c0; c < c1 && bad < 0; ++c) {
+        const double* col = h + (size_t)(c - c0) * (size_t)ldh;
+        double s2 = 0.0;
+        for (int i = 0; i <= c + 1; ++i) s2 += col[i] * col[i];
+        const double nrm = sqrt(s2);
+        ratio = nrm > 0.0 ? fabs(col[c + 1]) / nrm : 0.0;
+        if (!std::isfinite(s2) || nrm == 0.0 || ratio < kBreakdownTol) bad = c;
+    }
+    free(h);
+    if (flag) {
+        NKV_HIP(hipMemsetAsync(nan_flag_of(ws), 0, sizeof(int), st));
+        return fail(NKV_EBREAKDOWN, "breakdown: NaN in the factorisation (first suspect column %d)", bad);
+    }
+    if (bad >= 0)
+        return fail(NKV_EBREAKDOWN, "breakdown at column %d: |H(c+1,c)|/||H(:,c)|| = %.3g (invariant subspace)",
+                    bad, ratio);
+    return NKV_OK;
+}
+
 int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
                       int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec, void* mv_user,
                       nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream) {
@@ -2010,7 +2051,8 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
     }
     CHECK(nkv_dcgs2_coef(m, hd, nullptr, hd + m, H_dev, ldh, coef, ws, stream));
     CHECK(nkv_block_update(L, w, Q, m, hd, u, nullptr, ws, NKV_TIME, stream));
-    return nkv_normalize_dev(L, u, coef + 2 * m + 3, nullptr, 0, stream);
+    CHECK(nkv_normalize_dev(L, u, coef + 2 * m + 3, nullptr, 0, stream));
+    return (flags & NKV_CHECK_BREAKDOWN) ? check_breakdown(H_dev, ldh, mstart - 1, mend, ws, stream) : NKV_OK;
 }
 
 // update_hessenberg_matrix (krylov_decomposition.f90:103-189) as one call: the fused 3-pass CGS2
@@ -2036,6 +2078,20 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
         CHECK(reduce(nrm, 1, "norm"));
         return nkv_arnoldi_finish(L, f, nrm, q_out, 0, h1, nullptr, hcol_dev, 0, stream);
     }
+    if (flags & NKV_MGS2) {   // :155-186 in the reference's order; H(i,k) = alpha1 + alpha2 in finish
+        for (int pass = 0; pass < 2; ++pass) {
+            double* h = pass == 0 ? h1 : h2;
+            for (int i = 0; i < j; ++i) {
+                const double* qi = Q + (int64_t)i * L->ld;
+                CHECK(nkv_dot(L, w, f, qi, h + i, ws, tf, stream));
+                CHECK(reduce(h + i, 1, pass == 0 ? "first MGS pass" : "second MGS pass"));
+                CHECK(nkv_axpy_dev(L, f, h + i, -1.0, qi, NKV_TIME, stream));
+            }
+        }
+        CHECK(nkv_dot(L, w, f, f, nrm, ws, tf, stream));
+        CHECK(reduce(nrm, 1, "norm"));
+        return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
+    }
     CHECK(nkv_block_dot(L, w, Q, j, f, h1, ws, tf, stream));
     CHECK(reduce(h1, j, "first projection"));
     CHECK(nkv_block_update_dot(L, w, Q, j, h1, f, h2, ws, NKV_TIME | (tf ? NKV_TIME_DOT : 0u), stream));
@@ -2043,6 +2099,30 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
     CHECK(nkv_block_update(L, w, Q, j, h2, f, nrm, ws, NKV_TIME | NKV_NORM2 | tf, stream));
     CHECK(reduce(nrm, 1, "norm"));
     return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
+}
+
+// arnoldi_factorization (krylov_decomposition.f90:68-96) with the per-column update above: every
+// column final when its step ends (the cgs2 / mgs2 modes of nekstab_next_amd/arnoldi.py as one call).
+int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
+                              int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
+                              void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    if (!matvec) return fail(NKV_EINVAL, "matvec callback is NULL");
+    if (!H_dev || !scratch_dev) return fail(NKV_EINVAL, "H/scratch is NULL");
+    if (mstart < 1 || mend > NKV_MAX_COLS) return fail(NKV_EINVAL, "steps %d..%d outside 1..%d", mstart, mend, NKV_MAX_COLS);
+    if (mend < mstart) return NKV_OK;
+    if (ldh < mend + 1) return fail(NKV_EINVAL, "ldh=%lld < mend+1=%d", (long long)ldh, mend + 1);
+    const unsigned uf = flags & (NKV_TIME_DOT | NKV_MGS2);
+    for (int j = mstart; j <= mend; ++j) {   // f = A Q(j); orthonormalise against Q(1..j); Q(j+1) = f (:75-81)
+        double* x = Q + (int64_t)(j - 1) * L->ld;
+        const int rc = matvec(mv_user, x, f, stream);
+        if (rc != 0) return fail(NKV_ECALLBACK, "matvec callback returned %d at step %d", rc, j);
+        CHECK(nkv_update_hessenberg(L, w, Q, j, f, Q + (int64_t)j * L->ld, H_dev + (int64_t)(j - 1) * ldh, scratch_dev,
+                                    ws, allreduce, ar_user, uf, stream));
+    }
+    return (flags & NKV_CHECK_BREAKDOWN) ? check_breakdown(H_dev, ldh, mstart - 1, mend, ws, stream) : NKV_OK;
 }
 
 int nkv_arnoldi_finish(const nkv_layout* L, const double* f, const double* nrm2_dev, double* q_out,

@@ -49,6 +49,14 @@ class KrylovSchurResult:
     breakdowns: list = field(default_factory=list)        # mstart of each factorisation redone in MGS2
 
 
+_MGS2 = ("mgs2", "mgs2-native")
+
+
+def _mgs2_of(mode: str) -> str:
+    """The reference-order mode a solve falls back to: the library-driven one for a native mode."""
+    return "mgs2-native" if mode.endswith("-native") else "mgs2"
+
+
 def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float) -> int:
     """First Arnoldi column c in [c0, k) whose new direction vanished (|H(c+1,c)| < tol ||H(0:c+2,c)||,
     the Krylov space is invariant to rounding), or that holds a non-finite entry; -1 if none.
@@ -166,7 +174,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         graphs, lazy = None, False
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)
     while True:
-        if mode != "mgs2":
+        if mode not in _MGS2:
             H_before = H.copy()
             snap = snap if snap is not None else ctx.vector()
             snap.storage.copy_(Q.storage[mstart - 1])
@@ -180,10 +188,10 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
             H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
             ctx.check_nan()
         except NkvNaNError:
-            if mode == "mgs2":
+            if mode in _MGS2:
                 raise
             broken = True
-        if mode != "mgs2":
+        if mode not in _MGS2:
             broken = broken or breakdown_column(H, mstart - 1, k, cfg.breakdown_tol) >= 0
             if ctx.comm.world > 1:   # the H test is replicated; the NaN flag is per rank
                 flag = torch.tensor([1.0 if broken else 0.0], dtype=torch.float64, device=ctx.device)
@@ -196,7 +204,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
                 Q.storage[mstart - 1].copy_(snap.storage)
                 H[...] = H_before
                 Hd.upload(H)
-                mode, graphs, lazy = "mgs2", None, False
+                mode, graphs, lazy = _mgs2_of(mode), None, False
                 arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose,
                                       on_step=hook)
                 H[...] = Hd.download()
@@ -209,11 +217,11 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
             break
         schur_cnt += 1
         mstart, selected = schur_condensation(ctx, H, Q, k, cfg)
-        if ctx.time_in_dot and mode != "mgs2":
+        if ctx.time_in_dot and mode not in _MGS2:
             # the restart moves the fields but not `time` (eigensolvers.f90:421-432, 458-459), so
             # with time in k_dot (uparam(1)==2.1) the kept basis is no longer orthonormal: from here
             # on the reference's MGS2 order is mirrored (CGS2/DCGS2 assume an orthonormal basis)
-            mode, graphs, lazy = "mgs2", None, False
+            mode, graphs, lazy = _mgs2_of(mode), None, False
         res.mstart_history.append(mstart)
         res.selected_history.append(selected)
         Hd.upload(H)

@@ -267,7 +267,9 @@ def test_rotate_cols_row_bands(gpu, n_out):
 def test_native_dcgs2_driver_bit_identical(gpu, name):
     """nkv_arnoldi_dcgs2 (the whole DCGS2 factorisation in one ABI call, operator as a callback)
     gives the Python-driven DCGS2 factorisation bit for bit — from the seed and from mstart > 1 —
-    and nkv_update_hessenberg (one call per CGS2 column) the Python-driven CGS2 one."""
+    and nkv_arnoldi_factorization (per-column CGS2, or the reference's MGS2 order with NKV_MGS2) the
+    Python-driven CGS2 / MGS2 ones; so does nkv_update_hessenberg called per column (with a step
+    hook the native per-column modes run column by column)."""
     from nekstab_next_amd.layout import box3d_layout
 
     lay = box3d_layout(4000) if name == "large" else LAYOUTS[name]
@@ -276,15 +278,20 @@ def test_native_dcgs2_driver_bit_identical(gpu, name):
     op = DiagOperator(ctx, d)
     m = 20
     out = {}
-    for mode in ("dcgs2", "dcgs2-native", "cgs2", "cgs2-native"):
+    modes = ("dcgs2", "dcgs2-native", "cgs2", "cgs2-native", "cgs2-native-hook", "mgs2", "mgs2-native",
+             "mgs2-native-hook")
+    for mode in modes:
         Q = ctx.basis(m + 1)
         Q[0].fill_hash(5)
         k_normalize(Q[0])
         Hd = HessenbergDev(ctx, m)
-        arnoldi_factorization(ctx, op, Q, Hd, 1, 12, mode=mode)
-        arnoldi_factorization(ctx, op, Q, Hd, 13, m, mode=mode)   # continue from column 12 (mstart > 1)
+        hook = (lambda _s: None) if mode.endswith("-hook") else None
+        md = mode.replace("-hook", "")
+        arnoldi_factorization(ctx, op, Q, Hd, 1, 12, mode=md, on_step=hook)
+        arnoldi_factorization(ctx, op, Q, Hd, 13, m, mode=md, on_step=hook)   # continue from column 12
         out[mode] = (Hd.download(), Q.storage.cpu().numpy())
-    for a, b in (("dcgs2", "dcgs2-native"), ("cgs2", "cgs2-native")):
+    for a, b in (("dcgs2", "dcgs2-native"), ("cgs2", "cgs2-native"), ("cgs2", "cgs2-native-hook"),
+                 ("mgs2", "mgs2-native"), ("mgs2", "mgs2-native-hook")):
         np.testing.assert_array_equal(out[a][0], out[b][0])
         np.testing.assert_array_equal(out[a][1], out[b][1])
 
@@ -336,6 +343,81 @@ def test_native_dcgs2_driver_callback_errors(gpu):
     rc = ctx.lib.nkv_update_hessenberg(ctx._Lp, ctx.w.data_ptr(), Q.ptr, -1, f.ptr, Q.col_ptr(1), Hd.t.data_ptr(),
                                        scratch.data_ptr(), ctx.ws.data_ptr(), L_.ALLREDUCE_FN(), None, 0, ctx.stream)
     assert rc == L_.NKV_EINVAL
+    # the per-column one-call factorisation: the same argument checks and callback failure
+    for args, what in (((1, 4, 4, scratch.data_ptr()), "ldh"), ((0, 4, 5, scratch.data_ptr()), "outside"),
+                       ((1, 4, 5, None), "scratch")):
+        ms, me, ldh, scr = args
+        rc = ctx.lib.nkv_arnoldi_factorization(ctx._Lp, ctx.w.data_ptr(), Q.ptr, ms, me, Hd.t.data_ptr(), ldh, f.ptr,
+                                               scr, ctx.ws.data_ptr(), good, None, L_.ALLREDUCE_FN(), None,
+                                               L_.NKV_MGS2, ctx.stream)
+        assert rc == L_.NKV_EINVAL and what in L_.last_error(), (args, L_.last_error())
+    calls.clear()
+    rc = ctx.lib.nkv_arnoldi_factorization(ctx._Lp, ctx.w.data_ptr(), Q.ptr, 1, 4, Hd.t.data_ptr(), 5, f.ptr,
+                                           scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(bad), None,
+                                           L_.ALLREDUCE_FN(), None, L_.NKV_MGS2, ctx.stream)
+    assert rc == L_.NKV_ECALLBACK and "returned 7" in L_.last_error() and len(calls) == 1
+
+
+@pytest.mark.parametrize("rank", [3, 5])
+def test_native_breakdown_flag_and_mgs2_fallback(gpu, rank):
+    """NKV_CHECK_BREAKDOWN on the one-call drivers (include/nekkrylov.h, "Breakdown"): on a
+    rank-``rank`` operator nkv_arnoldi_dcgs2 returns NKV_EBREAKDOWN (its message names the column);
+    a C host then restores Q(mstart) and H and redoes the factorisation with
+    nkv_arnoldi_factorization(NKV_MGS2), without the flag (past the invariant subspace the noise
+    columns' ratios are tiny by construction; MGS2 normalises them as the reference does).  The
+    fallback's H and basis equal the Python-driven mgs2 factorisation bit for bit.  On a full-rank
+    operator the flag adds one synchronisation and returns NKV_OK with the same bits as without it."""
+    from nekstab_next_amd import _lib as L_
+    from nekstab_next_amd.arnoldi import _native_scratch
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    ctx, _ = make_ctx(lay, max_cols=32)
+    d = np.zeros(lay.ld)
+    for i in range(rank):
+        d[7 * (i + 1)] = 0.95 - 0.1 * i
+    m = 16
+    ops = {"deficient": DiagOperator(ctx, d), "full": DiagOperator(ctx, syn.diag_spectrum(lay)[0])}
+
+    def run_c(op, entry, flags, Q, Hd):
+        f = ctx.vector()
+        scratch = _native_scratch(ctx, m)
+        base, ld8 = Q.ptr, 8 * lay.ld
+
+        def mv(_u, x, y, _s):
+            op.matvec(Q[(x - base) // ld8], f)
+            return 0
+
+        return getattr(ctx.lib, entry)(ctx._Lp, ctx.w.data_ptr(), Q.ptr, 1, m, Hd.t.data_ptr(), m + 1, f.ptr,
+                                       scratch.data_ptr(), ctx.ws.data_ptr(), L_.MATVEC_FN(mv), None,
+                                       L_.ALLREDUCE_FN(), None, flags, ctx.stream)
+
+    def fresh():
+        Q = ctx.basis(m + 1)
+        Q[0].fill_hash(11)
+        k_normalize(Q[0])
+        return Q, HessenbergDev(ctx, m)
+
+    Q, Hd = fresh()
+    seed = Q.storage[0].clone()
+    rc = run_c(ops["deficient"], "nkv_arnoldi_dcgs2", L_.NKV_CHECK_BREAKDOWN, Q, Hd)
+    assert rc == L_.NKV_EBREAKDOWN, (rc, L_.last_error())
+    assert "breakdown" in L_.last_error()
+    ctx.check_nan()   # the driver cleared the NaN flag it reported
+    Q.storage[0].copy_(seed)   # restore, then the reference-order fallback
+    Hd.upload(np.zeros((m + 1, m), order="F"))
+    assert run_c(ops["deficient"], "nkv_arnoldi_factorization", L_.NKV_MGS2, Q, Hd) == L_.NKV_OK
+    Qp, Hp = fresh()
+    arnoldi_factorization(ctx, ops["deficient"], Qp, Hp, 1, m, mode="mgs2")
+    np.testing.assert_array_equal(Hd.download(), Hp.download())
+    np.testing.assert_array_equal(Q.storage.cpu().numpy(), Qp.storage.cpu().numpy())
+    # full rank: the flag returns NKV_OK, results unchanged
+    res = []
+    for flags in (0, L_.NKV_CHECK_BREAKDOWN):
+        Q, Hd = fresh()
+        assert run_c(ops["full"], "nkv_arnoldi_dcgs2", flags, Q, Hd) == L_.NKV_OK, L_.last_error()
+        res.append((Hd.download(), Q.storage.cpu().numpy()))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
 
 
 @pytest.mark.parametrize("mode", ["cgs2", "cgs2-unfused", "cgs2-native", "mgs2", "dcgs2", "dcgs2-lazy"])

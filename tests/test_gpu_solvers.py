@@ -473,7 +473,7 @@ def test_krylov_space_closing_early(gpu, mode):
 @pytest.mark.parametrize("rank", [3, 5])
 def test_invariant_subspace_breakdown_vs_oracle(gpu, mode, rank):
     """A rank-``rank`` operator (``rank`` nonzero diagonal entries 0.95, 0.85, ...) with k_dim=16: the
-    Krylov space is invariant after ``rank`` steps and every later vector is rounding noise.  Found by
+    Krylov space is invariant after ``rank`` + 1 steps and every later vector is rounding noise.  Found by
     tools/probe_breakdown.py: the one-pass classical forms fail there (DCGS2's Pythagorean norm goes
     negative -> NkvNaNError; CGS2 silently returned wrong Ritz values), while the reference's MGS2
     carries on.  The solver detects the breakdown (|H(c+1,c)| < 1e-8 ||H(:,c)||), redoes that
