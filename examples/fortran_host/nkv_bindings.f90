@@ -8,7 +8,8 @@ module nkv_bindings
 
    integer(c_int), parameter :: NKV_OK = 0, NKV_TILE = 4096
    integer(c_int), parameter :: NKV_TIME = 1, NKV_NORM2 = 8, NKV_OVERWRITE = 4, NKV_TIME_DOT = 16
-   integer(c_int), parameter :: NKV_X_IS_LAST = 32
+   integer(c_int), parameter :: NKV_X_IS_LAST = 32, NKV_MGS2 = 64, NKV_CHECK_BREAKDOWN = 128
+   integer(c_int), parameter :: NKV_ECALLBACK = 5, NKV_EBREAKDOWN = 6
 
    type, bind(C) :: nkv_layout
       integer(c_int64_t) :: n_v, n_p, sv, sp, ld
@@ -96,6 +97,16 @@ module nkv_bindings
       end function
       integer(c_int) function nkv_arnoldi_dcgs2(L, w, Q, mstart, mend, H, ldh, f, scratch, ws, matvec, mv_user, &
             allreduce, ar_user, flags, stream) bind(C, name="nkv_arnoldi_dcgs2")
+         import :: c_int, c_int64_t, c_ptr, c_funptr, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: w, Q, H, f, scratch, ws, mv_user, ar_user, stream
+         integer(c_int), value :: mstart, mend, flags
+         integer(c_int64_t), value :: ldh
+         type(c_funptr), value :: matvec, allreduce
+      end function
+      ! per-column factorisation (CGS2, or the reference's MGS2 order with NKV_MGS2): same arguments
+      integer(c_int) function nkv_arnoldi_factorization(L, w, Q, mstart, mend, H, ldh, f, scratch, ws, matvec, &
+            mv_user, allreduce, ar_user, flags, stream) bind(C, name="nkv_arnoldi_factorization")
          import :: c_int, c_int64_t, c_ptr, c_funptr, nkv_layout
          type(nkv_layout), intent(in) :: L
          type(c_ptr), value :: w, Q, H, f, scratch, ws, mv_user, ar_user, stream
