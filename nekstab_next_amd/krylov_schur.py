@@ -57,20 +57,22 @@ def _mgs2_of(mode: str) -> str:
     return "mgs2-native" if mode.endswith("-native") else "mgs2"
 
 
-def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float) -> int:
+def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float, offset: int = 1) -> int:
     """First Arnoldi column c in [c0, k) whose new direction vanished (|H(c+1,c)| < tol ||H(0:c+2,c)||,
     the Krylov space is invariant to rounding), or that holds a non-finite entry; -1 if none.
+    ``offset``: row of a column's new-direction norm relative to c (1 for Hessenberg H; 0 for the
+    upper-triangular projection C of Golub–Kahan–Lanczos, whose column c ends at alpha = C(c,c)).
 
     At such a step the reference's MGS2 (eigensolvers.f90:101-112) still produces a unit vector from the
     rounding noise, orthogonalised twice one projection at a time.  The one-pass classical forms cannot:
     CGS2 leaves O(eps/ratio) components in span(Q) (garbage at ratio ~ eps), and DCGS2's Pythagorean
     norm sqrt(||u||^2 - ||Q^T u||^2) cancels to a negative (NaN).  Normal runs sit at ratios >= 0.1."""
     for c in range(max(c0, 0), k):
-        col = H[:c + 2, c]
+        col = H[:c + 1 + offset, c]
         if not np.all(np.isfinite(col)):
             return c
         nrm = float(np.linalg.norm(col))
-        if nrm == 0.0 or abs(col[c + 1]) < tol * nrm:
+        if nrm == 0.0 or abs(col[c + offset]) < tol * nrm:
             return c
     return -1
 

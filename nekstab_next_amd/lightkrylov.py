@@ -28,7 +28,8 @@ import torch
 from . import lapack
 from .arnoldi import HessenbergDev, arnoldi_factorization, orthonormalize
 from .config import KrylovSchurConfig
-from .krylov_schur import krylov_schur
+from ._lib import NkvNaNError
+from .krylov_schur import _MGS2, _mgs2_of, breakdown_column, krylov_schur
 from .operators import LinearOperator
 from .vector import Basis, NekContext, NekVector, combine, k_add2, k_copy, k_matmul
 
@@ -92,24 +93,44 @@ class SvdsResult:
     residuals: np.ndarray  # beta_k |p_i(k)|
     info: int
     C: np.ndarray          # k x k upper-triangular projection A V_k = U_k C
+    breakdown: bool = False  # the bidiagonalisation reached an invariant subspace and was redone in MGS2
 
 
 def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, tolerance: float,
-         mode: str = "cgs2") -> SvdsResult:
+         mode: str = "cgs2", breakdown_tol: float = 1e-8) -> SvdsResult:
     """k-step Golub–Kahan–Lanczos bidiagonalisation with full re-orthogonalisation, k = len(U)-1.
-    V[0] holds the prepared (normalised) seed.  A: ``matvec`` (direct) and ``rmatvec`` (adjoint)."""
+    V[0] holds the prepared (normalised) seed.  A: ``matvec`` (direct) and ``rmatvec`` (adjoint).
+
+    A rank-deficient A makes the bidiagonalisation invariant before k steps (alpha_j or beta_j is
+    rounding noise).  As in ``krylov_schur`` the classical modes cannot carry on from noise, so
+    after the k steps the new-direction norms are checked (``breakdown_column``, |alpha_j| or
+    |beta_j| < ``breakdown_tol`` x its column, or a NaN) and the whole bidiagonalisation is redone in
+    the one-projection-at-a-time MGS2 order (V[0] is never written, so it needs no snapshot)."""
     k = U.k - 1
     if V.k < k + 1:
         raise ValueError("V must have as many vectors as U")
     Cd = HessenbergDev(ctx, k)   # columns: projections of A v_j on u_1..u_j (+ norm)
     Dd = HessenbergDev(ctx, k)   # columns: projections of A^T u_j on v_1..v_{j+1}
     f = ctx.vector()
-    for j in range(1, k + 1):
-        A.matvec(V[j - 1], f)
-        orthonormalize(ctx, U, j - 1, f, U.col_ptr(j - 1), Cd.col_ptr(j - 1), mode)
-        A.rmatvec(U[j - 1], f)
-        orthonormalize(ctx, V, j, f, V.col_ptr(j), Dd.col_ptr(j - 1), mode)
-    ctx.check_nan()
+    broken = False
+    while True:
+        for j in range(1, k + 1):
+            A.matvec(V[j - 1], f)
+            orthonormalize(ctx, U, j - 1, f, U.col_ptr(j - 1), Cd.col_ptr(j - 1), mode)
+            A.rmatvec(U[j - 1], f)
+            orthonormalize(ctx, V, j, f, V.col_ptr(j), Dd.col_ptr(j - 1), mode)
+        if mode in _MGS2:
+            ctx.check_nan()
+            break
+        try:
+            ctx.check_nan()
+            nan = False
+        except NkvNaNError:
+            nan = True
+        if not (nan or breakdown_column(Cd.download(), 0, k, breakdown_tol, offset=0) >= 0
+                or breakdown_column(Dd.download(), 0, k, breakdown_tol, offset=1) >= 0):
+            break
+        mode, broken = _mgs2_of(mode), True
     Ct = Cd.download()  # (k+1, k): column j-1 holds <u_i, A v_j> (i < j) and alpha_j at row j-1
     C = np.zeros((k, k))
     for j in range(k):
@@ -118,7 +139,7 @@ def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, toler
     P, s, Rt = np.linalg.svd(C)
     residuals = np.abs(beta_k * P[k - 1, :])
     info = 0 if int(np.count_nonzero(residuals < tolerance)) >= nev else 1
-    return SvdsResult(sigma=s, uvecs=P, vvecs=Rt.T, residuals=residuals, info=info, C=C)
+    return SvdsResult(sigma=s, uvecs=P, vvecs=Rt.T, residuals=residuals, info=info, C=C, breakdown=broken)
 
 
 def gmres(ctx: NekContext, A: LinearOperator, b: NekVector, x: NekVector, atol: float = 1e-12,

@@ -54,9 +54,39 @@ def test_svds_matches_dense_weighted_svd(gpu):
     prepare_seed(seed, V[0])
     r = svds(ctx, A, U, V, nev=3, tolerance=1e-8)
     conv = r.residuals < 1e-8
-    assert conv.sum() >= 3
+    assert conv.sum() >= 3 and not r.breakdown
     np.testing.assert_allclose(r.sigma[:3], s_exact[:3], rtol=1e-10)
     # singular triplet: A v = sigma u
+    u, v, Av = ctx.vector(), ctx.vector(), ctx.vector()
+    get_vec(u, U, r.uvecs[:, 0], k)
+    get_vec(v, V, r.vvecs[:, 0], k)
+    A.matvec(v, Av)
+    Av.axpby(1.0, u, -r.sigma[0])
+    assert np.sqrt(ctx.dot(Av, Av, False)) < 1e-9 * r.sigma[0]
+
+
+@pytest.mark.parametrize("mode", ["cgs2", "cgs2-native"])
+def test_svds_rank_deficient_breakdown(gpu, mode):
+    """A rank-3 operator (three nonzero diagonal entries, W-self-adjoint, so the singular values are
+    |d_i|) with k=12: the bidiagonalisation is invariant after 4 steps.  svds detects it (the
+    new-direction norms alpha_j / beta_j fall below 1e-8 of their columns), redoes it in MGS2 order
+    and returns the three exact singular values to 1e-10; the rest are rounding-level."""
+    w = syn.mass_weights(LAY)
+    ctx = NekContext(LAY, weights=w, max_cols=64)
+    d = np.zeros(LAY.ld)
+    exact = np.array([0.9, 0.6, 0.3])
+    for i, v in enumerate(exact):
+        d[7 * (i + 1)] = v
+    A = DiagOperator(ctx, d)
+    k = 12
+    U, V = ctx.basis(k + 1), ctx.basis(k + 1)
+    seed = ctx.vector()
+    seed.fill_hash(7)
+    prepare_seed(seed, V[0])
+    r = svds(ctx, A, U, V, nev=3, tolerance=1e-8, mode=mode)
+    assert r.breakdown
+    np.testing.assert_allclose(r.sigma[:3], exact, rtol=1e-10)
+    assert np.all(r.sigma[3:] < 1e-12)
     u, v, Av = ctx.vector(), ctx.vector(), ctx.vector()
     get_vec(u, U, r.uvecs[:, 0], k)
     get_vec(v, V, r.vvecs[:, 0], k)
