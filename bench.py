@@ -75,12 +75,16 @@ def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
     """HBM bytes the executed algorithm moves per factorisation (global sizes), per kernel:
     block_dot 8(jN_w + N_w + n_v); fused update_dot 8(jN + 2N + n_v); update+norm 8(jN + 2N + n_v);
     finish 8(2N); diag matvec 8(3N); DCGS2 dual update 8((j-1)N + 4N), over a lazy basis (one
-    output vector) 8(jN + 2N).  (PMC FETCH/WRITE_SIZE agree within 1%, profiles/.)"""
+    output vector) 8(jN + 2N); mgs2 (the reference's order) per column and pass a dot 8(2N_w + n_v)
+    and an axpy 8(3N), then the norm 8(N_w + n_v).  A "-native" mode moves the bytes of its twin."""
+    mode = mode.replace("-native", "")
     tot = 0.0
     for j in range(1, m + 1):
         dot = 8.0 * (j * N_w + N_w + n_v)
         upd = 8.0 * (j * N + 2 * N)
-        if mode == "cgs2":
+        if mode == "mgs2":
+            tot += 2 * j * 8.0 * (2 * N_w + n_v + 3 * N) + 8.0 * (N_w + n_v)
+        elif mode == "cgs2":
             tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
         elif mode == "cgs2-unfused":
             tot += 2 * dot + upd + (upd + 8.0 * n_v)
@@ -277,7 +281,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--E", type=int, default=44176, help="global elements (44,176 -> N=1.0e8)")
     ap.add_argument("--m", type=int, default=128)
-    ap.add_argument("--mode", default="dcgs2", help="dcgs2 (default) | cgs2 | cgs2-unfused")
+    ap.add_argument("--mode", default="dcgs2",
+                    help="dcgs2 (default) | cgs2 | cgs2-unfused | mgs2 (reference order) | dcgs2-native | "
+                         "cgs2-native | mgs2-native (the one-call C drivers)")
     ap.add_argument("--lazy-basis", action="store_true",
                     help="dcgs2 over a lazy basis Q = S T (one vector write less per step)")
     ap.add_argument("--cpu-E", type=int, default=11044, help="CPU baseline sample (11,044 -> N=2.5e7)")
@@ -486,8 +492,8 @@ def run(args):
           "allreduce_ms_per_factorisation_max_over_ranks": round(ar_max, 3),
           "allreduces_per_factorisation": (ar["launches"] // args.steps) if ar else 0,
           "gs_incl_allreduce_ms": round(gs_ms + ar_ms, 2),
-          "executed_gs_gbs": round(gs_exec / (gs_ms * 1e-3) / 1e9, 1),
-          "survey_headline_gbs": round(survey_gs / (gs_ms * 1e-3) / 1e9, 1),
+          "executed_gs_gbs": round(gs_exec / (gs_ms * 1e-3) / 1e9, 1) if gs_ms > 0 else None,
+          "survey_headline_gbs": round(survey_gs / (gs_ms * 1e-3) / 1e9, 1) if gs_ms > 0 else None,
           "last_step_ms": None if last_step_ms is None else round(last_step_ms, 3),
           "last_step_survey_gbs": None if last_step_ms is None else round(b_last / (last_step_ms * 1e-3) / 1e9, 1),
           "note": ("rank-0 shard unless *_over_ranks; events on the launch stream; allreduce = events around "
@@ -504,7 +510,9 @@ def run(args):
     # dominant kernel family (rank-local launches; bytes are this rank's shard)
     dom = max(("block_dot", "update_dot", "block_update", "block_dot2", "dcgs2_update"),
               key=lambda k: phases.get(k, {}).get("total_ms", 0.0))
-    ph = phases[dom]
+    # the native drivers launch inside one library call and mgs2 runs per-column dots: no
+    # kernel-family events in those modes (their kernels are in a rocprof trace), only `value`
+    ph = phases.get(dom, {"gbps": 0.0, "avg_ms": 0.0, "avg_bytes": 0.0, "launches": 0})
     achieved = ph["gbps"]
     traffic, tsrc = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
@@ -558,7 +566,7 @@ def run(args):
                 "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
                                 + " allreduce") if world > 1 else "single GPU",
             },
-            "roofline": {
+            "roofline": None if dom not in phases else {
                 "bound": "hbm",
                 "kernel": dom,
                 "achieved": round(achieved, 1),
