@@ -1252,6 +1252,16 @@ __global__ __launch_bounds__(kThreads) void k_rotate_mfma(double* __restrict__ Q
     }
 }
 
+// streaming rotation: U k-steps of 4 loaded per batch, the next batch's loads issued before this
+// batch's MFMAs (NKV_ROT_PIPE): +13 % at k = 128 with 64-128 kept columns (fewer registers, two
+// workgroups per CU), within 2-4 % elsewhere (profiles/r02az_tune_rot_pipe*.log)
+#ifndef NKV_ROT_U
+#define NKV_ROT_U 4
+#endif
+#ifndef NKV_ROT_PIPE
+#define NKV_ROT_PIPE 1
+#endif
+
 // ------------------------------------------------------------------------------------------
 // Restart rotation, streaming form (n_out <= 16*MB and V[:, 0:n_out] fits LDS): V is staged in
 // LDS once per workgroup; afterwards every wave streams its own NB x 16-row slabs of Q straight
@@ -1283,8 +1293,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int m = 0; m < MB; ++m) acc[nb][m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
-        for (int i0 = 0; i0 < k; i0 += 4 * U) {
-            double b[U][NB];
+        auto load = [&](double (&b)[U][NB], int i0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + 4 * u + lk;
@@ -1292,6 +1301,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) b[u][nb] = i < k ? qi[nb * 16] : 0.0;
             }
+        };
+        auto mma = [&](const double (&b)[U][NB], int i0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -1301,6 +1312,26 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
                     for (int nb = 0; nb < NB; ++nb)
                         acc[nb][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u][nb], acc[nb][m], 0, 0, 0);
                 }
+            }
+        };
+        if (NKV_ROT_PIPE) {   // the next batch's loads in flight while this batch's MFMAs issue
+            double b0[U][NB], b1[U][NB];   // two batches per trip: no register copies
+            load(b0, 0);
+            for (int i0 = 0;; i0 += 8 * U) {   // b0 holds the batch at i0 < k (wave-uniform branches)
+                const bool more1 = i0 + 4 * U < k;
+                if (more1) load(b1, i0 + 4 * U);
+                mma(b0, i0);
+                if (!more1) break;
+                const bool more2 = i0 + 8 * U < k;
+                if (more2) load(b0, i0 + 8 * U);
+                mma(b1, i0 + 4 * U);
+                if (!more2) break;
+            }
+        } else {
+            for (int i0 = 0; i0 < k; i0 += 4 * U) {
+                double b[U][NB];
+                load(b, i0);
+                mma(b, i0);
             }
         }
 #pragma unroll
@@ -1312,6 +1343,94 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
 #pragma unroll
                     for (int nb = 0; nb < NB; ++nb) Q[(int64_t)gc * ld + row0 + nb * 16 + lr] = acc[nb][m][r];
                 }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Restart rotation, V streamed through LDS in k-chunks (n_out <= 16*MB <= 256 when V[:, 0:n_out]
+// does not fit LDS whole: k > 128 with many kept columns, where the staged tile kernel above keeps
+// one workgroup per CU and exposes every load).  As k_rotate_stream, every wave owns one 16-row
+// slab and holds all of its n_out outputs in registers until its k inputs are consumed (in place
+// is safe); V moves through two LDS buffers of KC k-rows (next chunk's V and Q loads in flight
+// while this chunk's MFMAs issue, one barrier per chunk).  LDS: Vs[buf][c][i], stride KP = 2
+// (mod 32) doubles as in k_rotate_stream.
+// ------------------------------------------------------------------------------------------
+template <int MB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_rotate_chunked(double* __restrict__ Q, int64_t ld, int k,
+                                                               const double* __restrict__ V, int ldv, int n_out,
+                                                               int64_t n_tiles) {
+    constexpr int KC = MB > 8 ? 16 : 32, KP = 34, U = KC / 4;
+    constexpr int VN = MB * 16 * KC, NT = WAVES * 64, PER = (VN + NT - 1) / NT;
+    constexpr int BUF = MB * 16 * KP;
+    extern __shared__ __attribute__((aligned(16))) double Vs[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int nchunks = (k + KC - 1) / KC;
+    auto vload = [&](double (&r)[PER], int kc) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int e = threadIdx.x + p * NT, c = e / KC, gi = kc + e % KC;
+            r[p] = (e < VN && gi < k && c < n_out) ? V[gi + (int64_t)c * ldv] : 0.0;
+        }
+    };
+    auto vstore = [&](const double (&r)[PER], int buf) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int e = threadIdx.x + p * NT;
+            if (e < VN) Vs[buf * BUF + (e / KC) * KP + e % KC] = r[p];
+        }
+    };
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t row0 = (tile * WAVES + wave) * 16;
+        const double* q = Q + row0 + lr;
+        auto bload = [&](double (&b)[U], int kc) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = kc + 4 * u + lk;
+                b[u] = i < k ? q[(int64_t)i * ld] : 0.0;
+            }
+        };
+        nkv_f64x4 acc[MB];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) acc[m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
+        double vr[PER], b[U];
+        vload(vr, 0);
+        bload(b, 0);
+        vstore(vr, 0);
+        __syncthreads();
+        for (int ch = 0; ch < nchunks; ++ch) {
+            const int cur = ch & 1;
+            const bool more = ch + 1 < nchunks;
+            double bn[U];
+            if (more) {
+                vload(vr, (ch + 1) * KC);
+                bload(bn, (ch + 1) * KC);
+            }
+            const double* vs = Vs + cur * BUF + lr * KP + lk;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(vs[m * 16 * KP + 4 * u], b[u], acc[m], 0, 0, 0);
+                // keep the next k-step's MB operand reads from being hoisted here: MB x 4 accumulators
+                // plus one k-step of A operands fit the register file, all U k-steps at once do not
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (more) {
+                vstore(vr, cur ^ 1);   // that buffer's readers passed the previous chunk's barrier
+#pragma unroll
+                for (int u = 0; u < U; ++u) b[u] = bn[u];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gc = m * 16 + lk + 4 * r;
+                if (gc < n_out) Q[(int64_t)gc * ld + row0 + lr] = acc[m][r];
             }
         }
     }
@@ -2258,9 +2377,7 @@ static int rotate_valu(const nkv_layout* L, double* Q, int k, const double* V_de
 #ifndef NKV_ROT_NB
 #define NKV_ROT_NB 1
 #endif
-#ifndef NKV_ROT_U
-#define NKV_ROT_U 8   // k-steps of 4 loaded per batch
-#endif
+
 
 extern "C++" template <int MB>
 static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
@@ -2283,6 +2400,33 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
     const int64_t g = n_tiles < g0 ? n_tiles : g0;
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, kp,
                        n_tiles);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+#ifndef NKV_ROT_CHUNKED
+#define NKV_ROT_CHUNKED 1   // 0: the staged tile kernel where V does not fit LDS whole
+#endif
+
+extern "C++" template <int MB>
+static int launch_rotate_chunked(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
+                                 void* stream) {
+    // 8 or more 16-column blocks: 4 x MB accumulators need one wave per SIMD (512 registers)
+    constexpr int W = MB >= 8 ? 4 : 8;
+    auto kern = k_rotate_chunked<MB, W>;
+    const size_t lds = 2 * (size_t)MB * 16 * 34 * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NKV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    const int64_t n_tiles = rows_of(L) / (W * 16);
+    if (n_tiles < 1) return NKV_OK;
+    int per_cu = (int)((160 * 1024) / lds);
+    per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
+    const int64_t g0 = (int64_t)device_cus() * per_cu;
+    const int64_t g = n_tiles < g0 ? n_tiles : g0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, n_tiles);
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -2356,6 +2500,14 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
                 default: break;
             }
         }
+    }
+    if (NKV_ROT_CHUNKED && rows_of(L) % (8 * 16) == 0) {   // V through LDS in k-chunks, n_out <= 256
+        const int nact = (n_out + 15) / 16;
+        if (nact <= 2) return launch_rotate_chunked<2>(L, Q, k, V_dev, ldv, n_out, stream);
+        if (nact <= 4) return launch_rotate_chunked<4>(L, Q, k, V_dev, ldv, n_out, stream);
+        if (nact <= 8) return launch_rotate_chunked<8>(L, Q, k, V_dev, ldv, n_out, stream);
+        if (nact <= 12) return launch_rotate_chunked<12>(L, Q, k, V_dev, ldv, n_out, stream);
+        if (nact <= 16) return launch_rotate_chunked<16>(L, Q, k, V_dev, ldv, n_out, stream);
     }
     if (k <= 256) {
         if (NKV_ROT_SMALLR == 32) return launch_rotate_mfma<32, 128, 16>(L, Q, k, V_dev, ldv, n_out, stream);

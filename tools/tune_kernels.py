@@ -44,6 +44,13 @@ VARIANTS = {
     "rot_w8_nb2": {"NKV_ROT_WAVES": 8, "NKV_ROT_NB": 2},
     "rot_u2": {"NKV_ROT_U": 2},
     "rot_u8": {"NKV_ROT_U": 8},
+    "rot_nopipe_u8": {"NKV_ROT_PIPE": 0, "NKV_ROT_U": 8},   # the round-2 streaming rotation before r02az
+    "rot_pipe": {"NKV_ROT_PIPE": 1},
+    "rot_pipe_u4": {"NKV_ROT_PIPE": 1, "NKV_ROT_U": 4},
+    "rot_u4": {"NKV_ROT_U": 4},
+    "rot_pipe_u2": {"NKV_ROT_PIPE": 1, "NKV_ROT_U": 2},
+    "rot_nochunk": {"NKV_ROT_CHUNKED": 0},
+    "rot_old": {"NKV_ROT_PIPE": 0, "NKV_ROT_U": 8, "NKV_ROT_CHUNKED": 0},   # rotation kernels before r02az
     "dc_u4": {"NKV_DC_U": 4},
     "dc_p4": {"NKV_DC_PAIRS": 4},
     "dc_p4_u4": {"NKV_DC_PAIRS": 4, "NKV_DC_U": 4, "NKV_D2_U": 4},
@@ -217,6 +224,10 @@ def run(names, E, rounds, js, only=None):
                           8.0 * (j + min(16, j)) * N),
             "rotate_32": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(32, j), st),
                           8.0 * (j + min(32, j)) * N),
+            "rotate_64": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(64, j), st),
+                          8.0 * (j + min(64, j)) * N),
+            "rotate_half": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 2), st),
+                            8.0 * (j + max(1, j // 2)) * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
                             8.0 * (j + max(1, j // 6)) * N),
         }
