@@ -2407,6 +2407,9 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
 #ifndef NKV_ROT_CHUNKED
 #define NKV_ROT_CHUNKED 1   // 0: the staged tile kernel where V does not fit LDS whole
 #endif
+#ifndef NKV_ROT_CHUNK_FROM
+#define NKV_ROT_CHUNK_FROM 17   // 16-column blocks from which the chunked kernel replaces the streaming one
+#endif
 
 extern "C++" template <int MB>
 static int launch_rotate_chunked(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
@@ -2483,7 +2486,8 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
             default: break;
         }
     }
-    if (NKV_ROT_STREAM && rows_of(L) % ((int64_t)NKV_ROT_WAVES * NKV_ROT_NB * 16) == 0) {
+    if (NKV_ROT_STREAM && (n_out + 15) / 16 < NKV_ROT_CHUNK_FROM &&
+        rows_of(L) % ((int64_t)NKV_ROT_WAVES * NKV_ROT_NB * 16) == 0) {
         const int kp = ((k + 31) & ~31) + 2;
         const int nact = (n_out + 15) / 16;
         const size_t lds = (size_t)nact * 16 * kp * sizeof(double);
