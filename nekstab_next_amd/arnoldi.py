@@ -341,8 +341,12 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     """k-step Arnoldi from column ``mstart`` to ``mend`` (1-based, inclusive), as
     krylov_decomposition.f90:68-96: f = A q_mstep; orthonormalise; Q(mstep+1) = f.
 
-    ``on_step(mstep)`` is called after each step (hook for checkpointing, cf. ifres at :84); it
-    needs the finished column after every step, so with a hook ``"dcgs2"`` runs as ``"cgs2"``.
+    ``on_step(mstep)`` is called once column mstep (0-based: Q[mstep], the reference's Q(mstep+1))
+    and H columns 0..mstep-1 are final (hook for checkpointing, cf. ifres at :84).  CGS2 and MGS2
+    finish each column in its own step.  DCGS2 finishes column j-1 in step j, so its hook for
+    mstep = j-1 runs right after step j (one step later than the reference's call at :84, with the
+    same content), and the hook for mend after the closing pass; ``"dcgs2-native"`` with a hook
+    runs this Python-driven DCGS2.
 
     ``lazy=True`` (``"dcgs2"`` only): the finished columns are left as Q = S T (see ``Basis``) —
     one vector write less per step; on return ``Q.lazy = mend`` (column mend is final).  The
@@ -361,6 +365,18 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
             _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose)
             return
         mode = "dcgs2"
+    if mode == "dcgs2" and on_step is not None:   # lagged hooks: column j-1 is final after step j
+        if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+            raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        _settle_basis(Q, mstart, lazy=False)
+        for mstep in range(mstart, mend + 1):
+            (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
+            _dcgs2_step(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
+            if mstep > mstart:
+                on_step(mstep - 1)
+        _dcgs2_close(ctx, Q, Hd, mend)
+        on_step(mend)
+        return
     if mode in ("cgs2-native", "mgs2-native") and on_step is None:   # per-column modes, one ABI call
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")

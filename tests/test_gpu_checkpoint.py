@@ -74,3 +74,40 @@ def test_outpost_ks_files(gpu, tmp_path):
         re = ctx.vector().from_packed(fld.vector_from_fld(lay, fld.read_fld(str(tmp_path / fld.fld_name("dRe", "nek", 0, num)))))
         im = ctx.vector().from_packed(fld.vector_from_fld(lay, fld.read_fld(str(tmp_path / fld.fld_name("dIm", "nek", 0, num)))))
         assert abs(ctx.dot(re, re, False) + ctx.dot(im, im, False) - 1.0) < 1e-10
+
+
+def test_dcgs2_step_hook_sees_final_columns(gpu):
+    """DCGS2 with a per-step hook (checkpointing): the hook for step k runs once column k of Q and
+    H's columns 0..k-1 are final — every step mstart..k_dim of every Krylov–Schur cycle, in order —
+    and what it sees equals the end of the factorisation bit for bit; the hook changes nothing
+    (the whole solve equals the hook-free DCGS2 solve bit for bit)."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), max_cols=32)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    k = 16
+    cfg = KrylovSchurConfig(k_dim=k, schur_tgt=5, mode="dcgs2")
+    ref = krylov_schur(ctx, op, seed, cfg)
+    Qref = ref.Q.storage.cpu().numpy().copy()
+    seen = []
+
+    def hook(mstep, Q, Hd):
+        seen.append((mstep, Hd.download()[: mstep + 1, :mstep].copy(), Q.storage[mstep].cpu().numpy().copy()))
+
+    cycles = []
+    res = krylov_schur(ctx, op, seed, cfg, on_step=hook,
+                       on_restart=lambda cnt, ms: cycles.append((len(seen), ms)))
+    assert res.schur_cnt == ref.schur_cnt and res.mstart_history == ref.mstart_history
+    np.testing.assert_array_equal(res.H, ref.H)
+    np.testing.assert_array_equal(res.Q.storage.cpu().numpy(), Qref)
+    # the step sequence: 1..k, then mstart..k after each restart
+    starts = [1] + res.mstart_history
+    want = [s for m in starts for s in range(m, k + 1)]
+    assert [s for s, _, _ in seen] == want
+    # within the last factorisation the hook's view is the final state (earlier cycles were rotated)
+    last = len(seen) - (k - starts[-1] + 1)
+    for mstep, Hs, q in seen[last:]:
+        np.testing.assert_array_equal(Hs, res.H[: mstep + 1, :mstep])
+        np.testing.assert_array_equal(q, Qref[mstep])
