@@ -51,6 +51,8 @@ VARIANTS = {
     "rot_pipe_u2": {"NKV_ROT_PIPE": 1, "NKV_ROT_U": 2},
     "rot_nochunk": {"NKV_ROT_CHUNKED": 0},
     "rot_chunk5": {"NKV_ROT_CHUNK_FROM": 5},
+    "rot_nb2": {"NKV_ROT_NB": 2},
+    "rot_nb2_w8": {"NKV_ROT_NB": 2, "NKV_ROT_WAVES": 8},
     "rot_w8u8": {"NKV_ROT_WAVES": 8, "NKV_ROT_U": 8},
     "rot_old": {"NKV_ROT_PIPE": 0, "NKV_ROT_U": 8, "NKV_ROT_CHUNKED": 0},   # rotation kernels before r02az
     "dc_u4": {"NKV_DC_U": 4},
