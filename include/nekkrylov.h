@@ -246,7 +246,8 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
  * runs sit at ratios >= 0.1.  nkv_arnoldi_dcgs2 has by then rewritten Q column mstart-1 and H row
  * mstart-1 (the delayed re-orthogonalisation of the seed column): the caller restores both from its
  * own copies and redoes the factorisation with nkv_arnoldi_factorization(..., NKV_MGS2, ...), as
- * nekstab_next_amd.krylov_schur does. */
+ * nekstab_next_amd.krylov_schur does.  H is replicated, so every rank reaches the same ratio test;
+ * the NaN flag is per rank, so a sharded host all-reduces its breakdown decision before branching. */
 int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
                               int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
                               void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
