@@ -1348,6 +1348,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     }
 }
 
+#ifndef NKV_ROT_CHUNK_SB
+#define NKV_ROT_CHUNK_SB 1
+#endif
+#ifndef NKV_ROT_CHUNK_W8_MAX
+#define NKV_ROT_CHUNK_W8_MAX 8   // chunked rotation: 8 waves up to this many 16-column blocks (+12 % at
+                                 // 8 blocks over 4 waves, profiles/r02bf_tune_rot_w8.log), 4 above
+#endif
+
 // ------------------------------------------------------------------------------------------
 // Restart rotation, V streamed through LDS in k-chunks (n_out <= 16*MB <= 256 when V[:, 0:n_out]
 // does not fit LDS whole: k > 128 with many kept columns, where the staged tile kernel above keeps
@@ -1414,9 +1422,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_chunked(double* __restric
 #pragma unroll
                 for (int m = 0; m < MB; ++m)
                     acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(vs[m * 16 * KP + 4 * u], b[u], acc[m], 0, 0, 0);
-                // keep the next k-step's MB operand reads from being hoisted here: MB x 4 accumulators
-                // plus one k-step of A operands fit the register file, all U k-steps at once do not
-                __builtin_amdgcn_sched_barrier(0);
+                // 8 waves (256 registers each): keep the next k-step's MB operand reads from being
+                // hoisted here — MB x 4 accumulators plus one k-step of A operands fit, all U k-steps
+                // at once do not.  4 waves (512 registers): NKV_ROT_CHUNK_SB chooses.
+                if (WAVES > 4 || NKV_ROT_CHUNK_SB) __builtin_amdgcn_sched_barrier(0);
             }
             if (more) {
                 vstore(vr, cur ^ 1);   // that buffer's readers passed the previous chunk's barrier
@@ -2414,8 +2423,9 @@ static int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const dou
 extern "C++" template <int MB>
 static int launch_rotate_chunked(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
                                  void* stream) {
-    // 8 or more 16-column blocks: 4 x MB accumulators need one wave per SIMD (512 registers)
-    constexpr int W = MB >= 8 ? 4 : 8;
+    // past NKV_ROT_CHUNK_W8_MAX 16-column blocks the 4 x MB accumulators need one wave per SIMD
+    // (512 registers)
+    constexpr int W = MB > NKV_ROT_CHUNK_W8_MAX ? 4 : 8;
     auto kern = k_rotate_chunked<MB, W>;
     const size_t lds = 2 * (size_t)MB * 16 * 34 * sizeof(double);
     static bool attr_set = false;

@@ -209,7 +209,7 @@ def test_rotate_vs_oracle(gpu, k):
 
 @pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 6), (128, 8), (9, 9), (4, 4), (131, 5), (576, 7),
                                      (128, 12), (130, 13), (64, 16), (1000, 11), (128, 20), (129, 17), (256, 255),
-                                     (300, 150), (576, 33), (900, 6)])
+                                     (300, 150), (576, 33), (900, 6), (256, 100), (200, 128), (576, 256)])
 def test_rotate_cols_vs_oracle(gpu, k, n_out):
     """Partial restart rotation: Q[:, :n_out] = Q[:, :k] V[:, :n_out]; columns n_out..k untouched."""
     lay = LAYOUTS["2d"]

@@ -52,6 +52,8 @@ VARIANTS = {
     "rot_nochunk": {"NKV_ROT_CHUNKED": 0},
     "rot_chunk5": {"NKV_ROT_CHUNK_FROM": 5},
     "rot_nb2": {"NKV_ROT_NB": 2},
+    "rot_chunk_nosb": {"NKV_ROT_CHUNK_SB": 0},
+    "rot_chunk_w8": {"NKV_ROT_CHUNK_W8_MAX": 8},
     "rot_nb2_w8": {"NKV_ROT_NB": 2, "NKV_ROT_WAVES": 8},
     "rot_w8u8": {"NKV_ROT_WAVES": 8, "NKV_ROT_U": 8},
     "rot_old": {"NKV_ROT_PIPE": 0, "NKV_ROT_U": 8, "NKV_ROT_CHUNKED": 0},   # rotation kernels before r02az
