@@ -73,6 +73,12 @@ namespace {
                       // faster than 4 per CU at N=1e8 and at the 8-GPU shard; non-multiples of the
                       // 256 CUs lose 5-10 % (profiles/r01k_tune_update_grid.log)
 #endif
+#ifndef NKV_UPD_ROUNDS
+#define NKV_UPD_ROUNDS 2  // block update (CGS2 passes, DCGS2 close): row-band launches of this many rounds
+#endif                    // (+2 % on update+norm at N=1e8, profiles/r02bh_tune_upd_bands.log)
+#ifndef NKV_FUSE_ROUNDS
+#define NKV_FUSE_ROUNDS 0  // fused CGS2 middle pass: row-band launches of this many rounds (0: one launch)
+#endif
 #ifndef NKV_DC_ROUNDS
 #define NKV_DC_ROUNDS 2  // DCGS2 updates: one launch per this many grid-stride rounds of row tiles (a
                          // "row band"); the launch boundaries keep the grid's loads and stores in one
@@ -376,7 +382,8 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
                                                            int tiles_per_field, int tiles_w,
                                                            int tiles_total, int64_t time_off,
                                                            int do_time,
-                                                           double* __restrict__ partials) {
+                                                           double* __restrict__ partials, int t_lo,
+                                                           int acc_part) {
     constexpr int kTile = kThreads * kPairs * 2;
     __shared__ double lds4[4];
     // time slot (one double): wave 0 of block 0, lanes split the columns.
@@ -387,7 +394,7 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
         if (threadIdx.x == 0) f[time_off] = OVERWRITE ? s : f[time_off] - s;
     }
     double nrm = 0.0;
-    for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+    for (int t = t_lo + blockIdx.x; t < tiles_total; t += gridDim.x) {   // tiles t_lo..tiles_total-1
         const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
         double2 acc[kPairs];
 #pragma unroll
@@ -434,9 +441,9 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
             }
         }
     }
-    if (NORM) {
+    if (NORM) {   // a row band after the first adds to the block's partial (fixed order: deterministic)
         nrm = block_sum(nrm, lds4);
-        if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+        if (threadIdx.x == 0) partials[blockIdx.x] = acc_part ? partials[blockIdx.x] + nrm : nrm;
     }
 }
 
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
                                                          int64_t tiles_per_field, int64_t tiles_w,
                                                          int64_t tiles_total, int64_t time_off,
                                                          int do_time, double* __restrict__ partials,
-                                                         int B) {
+                                                         int B, int64_t t_lo, int acc_part) {
     __shared__ double2 part[2][NW][64];  // double-buffered: one barrier per tile
     // wave index made provably uniform: column bases become scalar registers, the per-lane part of
     // every address is one 32-bit row offset
@@ -490,7 +497,7 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
         q[CPW - 1] = (wv + NW * (CPW - 1) < j) ? ldq(at_b(qcol[CPW - 1], rb)) : make_double2(0.0, 0.0);
     };
     double2 q[CPW];
-    for (int64_t t = blockIdx.x; t < tiles_total; t += gridDim.x, buf ^= 1) {
+    for (int64_t t = t_lo + blockIdx.x; t < tiles_total; t += gridDim.x, buf ^= 1) {   // tiles t_lo..
         const uint32_t r = (uint32_t)(t * kFuseRows) + 2u * lane;
         load_tile(q, t);
         double2 s = make_double2(0.0, 0.0);
@@ -527,7 +534,8 @@ __global__ __launch_bounds__(NW * 64) void k_update_dot(const double* __restrict
     for (int i = 0; i < CPW; ++i) {
         const int c = wv + NW * i;
         const double v = wave_sum(acc[i]);
-        if (lane == 0 && c < j) partials[(int64_t)c * B + blockIdx.x] = v;
+        if (lane == 0 && c < j)   // a row band after the first adds to the block's partials (fixed order)
+            partials[(int64_t)c * B + blockIdx.x] = acc_part ? partials[(int64_t)c * B + blockIdx.x] + v : v;
     }
 }
 
@@ -1699,15 +1707,20 @@ int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q,
     *g_out = g;
     const int64_t T = rows_of(L);
     const int dt = (flags & NKV_TIME) ? 1 : 0;
-    if (over && norm)
-        hipLaunchKernelGGL((k_block_update<true, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (over)
-        hipLaunchKernelGGL((k_block_update<true, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else if (norm)
-        hipLaunchKernelGGL((k_block_update<false, true, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    else
-        hipLaunchKernelGGL((k_block_update<false, false, P>), dim3(g), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, tiles_total, T, dt, part);
-    NKV_LAUNCHED();
+    auto kern = over ? (norm ? k_block_update<true, true, P> : k_block_update<true, false, P>)
+                     : (norm ? k_block_update<false, true, P> : k_block_update<false, false, P>);
+    // NKV_UPD_ROUNDS > 0: one launch per row band of that many grid-stride rounds, as the DCGS2
+    // updates (the first band launches the whole grid, so every block's partial slot is written)
+    const int64_t b = (int64_t)NKV_UPD_ROUNDS * g;
+    const int band = (NKV_UPD_ROUNDS <= 0 || b >= tiles_total || tiles_total < 2 * b) ? (tiles_total > 0 ? tiles_total : 1)
+                                                                                        : (int)b;
+    for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {
+        const int hi = lo + band < tiles_total ? lo + band : tiles_total;
+        const int gb = lo == 0 ? g : (g < hi - lo ? g : hi - lo);
+        hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, Q, L->ld, j, h_dev, f, w, L->sv, tpf, tiles_w, hi, T,
+                           lo == 0 ? dt : 0, part, lo, lo == 0 ? 0 : 1);
+        NKV_LAUNCHED();
+    }
     return NKV_OK;
 }
 
@@ -1897,9 +1910,18 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
     hipStream_t st = S(stream);
-#define NKV_FUSE(NW, CPW)                                                                                     \
-    hipLaunchKernelGGL((k_update_dot<NW, CPW>), dim3((unsigned)g), dim3(NW * 64), 0, st, Q, L->ld, j, h_dev, f, w, \
-                       L->sv, tpf, tiles_w, tiles_total, T, dt, part, B)
+    // NKV_FUSE_ROUNDS > 0: one launch per row band of that many grid-stride rounds (the first band
+    // launches the whole grid, so every partial slot is written before later bands add to it)
+    const int64_t fb = (int64_t)NKV_FUSE_ROUNDS * g;
+    const int64_t fband = (NKV_FUSE_ROUNDS <= 0 || fb >= tiles_total || tiles_total < 2 * fb)
+                              ? (tiles_total > 0 ? tiles_total : 1) : fb;   // >= 1: an empty shard launches once
+#define NKV_FUSE(NW, CPW)                                                                                        \
+    for (int64_t lo = 0; lo == 0 || lo < tiles_total; lo += fband) {                                             \
+        const int64_t hi = lo + fband < tiles_total ? lo + fband : tiles_total;                                  \
+        const int64_t gb = lo == 0 ? g : (g < hi - lo ? g : hi - lo);                                            \
+        hipLaunchKernelGGL((k_update_dot<NW, CPW>), dim3((unsigned)gb), dim3(NW * 64), 0, st, Q, L->ld, j, h_dev, f, \
+                           w, L->sv, tpf, tiles_w, hi, T, lo == 0 ? dt : 0, part, B, lo, lo == 0 ? 0 : 1);        \
+    }
     constexpr int NW = NKV_FUSE_NW;
     const int cpw = j <= NW * 16 ? (j + NW - 1) / NW : (j + 15) / 16;
     if (j <= NW * 16) {

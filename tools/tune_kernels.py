@@ -52,6 +52,13 @@ VARIANTS = {
     "rot_nochunk": {"NKV_ROT_CHUNKED": 0},
     "rot_chunk5": {"NKV_ROT_CHUNK_FROM": 5},
     "rot_nb2": {"NKV_ROT_NB": 2},
+    "upd_r1": {"NKV_UPD_ROUNDS": 1},
+    "upd_r2": {"NKV_UPD_ROUNDS": 2},
+    "upd_r4": {"NKV_UPD_ROUNDS": 4},
+    "upd_r0": {"NKV_UPD_ROUNDS": 0},   # the single-launch update before r02bh
+    "fuse_r1": {"NKV_FUSE_ROUNDS": 1},
+    "fuse_r2": {"NKV_FUSE_ROUNDS": 2},
+    "fuse_r4": {"NKV_FUSE_ROUNDS": 4},
     "rot_chunk_nosb": {"NKV_ROT_CHUNK_SB": 0},
     "rot_chunk_w8": {"NKV_ROT_CHUNK_W8_MAX": 8},
     "rot_nb2_w8": {"NKV_ROT_NB": 2, "NKV_ROT_WAVES": 8},
