@@ -75,15 +75,15 @@ def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
     """HBM bytes the executed algorithm moves per factorisation (global sizes), per kernel:
     block_dot 8(jN_w + N_w + n_v); fused update_dot 8(jN + 2N + n_v); update+norm 8(jN + 2N + n_v);
     finish 8(2N); diag matvec 8(3N); DCGS2 dual update 8((j-1)N + 4N), over a lazy basis (one
-    output vector) 8(jN + 2N); mgs2 (the reference's order) per column and pass a dot 8(2N_w + n_v)
-    and an axpy 8(3N), then the norm 8(N_w + n_v).  A "-native" mode moves the bytes of its twin."""
+    output vector) 8(jN + 2N); mgs2 (the reference's order) one dot 8(2N_w + n_v), then per column
+    and pass one fused axpy + next dot (nkv_axpy_dot) 8(3N + N_w + n_v), the last one's dot the norm.  A "-native" mode moves the bytes of its twin."""
     mode = mode.replace("-native", "")
     tot = 0.0
     for j in range(1, m + 1):
         dot = 8.0 * (j * N_w + N_w + n_v)
         upd = 8.0 * (j * N + 2 * N)
-        if mode == "mgs2":
-            tot += 2 * j * 8.0 * (2 * N_w + n_v + 3 * N) + 8.0 * (N_w + n_v)
+        if mode == "mgs2":   # a dot, then 2j fused column passes (the last one's dot is ||f||^2)
+            tot += 8.0 * (2 * N_w + n_v) + 2 * j * 8.0 * (3 * N + N_w + n_v) - 8.0 * N_w
         elif mode == "cgs2":
             tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
         elif mode == "cgs2-unfused":

@@ -164,6 +164,14 @@ int nkv_normalize_store(const nkv_layout* L, const double* f, const double* nrm2
                         double* beta_dev, unsigned flags, void* stream);
 int nkv_mgs2_step(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
                   double* hcol_dev, void* ws, unsigned flags, void* stream);
+/* One column of an MGS pass fused with the next one's projection (update_hessenberg_matrix's
+ * k_cmult + k_sub2 then k_dot, krylov_decomposition.f90:157-166 / :173-180, in that order):
+ *   f <- f - (*alpha_dev) qa                 (NKV_TIME: the time slot too, as k_sub2)
+ *   *out_dev = <f_new, qb>_W  LOCAL partial  (qb = NULL: <f_new, f_new>, the closing k_normalize);
+ * NKV_TIME_DOT adds the time product (rank0).  One read of f for the pair of operations; the MGS2
+ * sequences of nkv_update_hessenberg(NKV_MGS2) and nkv_mgs2_step are built from it. */
+int nkv_axpy_dot(const nkv_layout* L, const double* w, double* f, const double* alpha_dev, const double* qa,
+                 const double* qb, double* out_dev, void* ws, unsigned flags, void* stream);
 
 /* ---- DCGS2: classical Gram–Schmidt with delayed re-orthogonalisation (two reads of Q per step,
  * ONE all-reduce per step, no separate normalisation pass).  Same replacement target as the CGS2

@@ -96,6 +96,7 @@ _SIGNATURES = {
     "nkv_combine": (c_int, [_L, _P, c_int, _P, _P, c_uint, _P]),
     "nkv_normalize_store": (c_int, [_L, _P, _P, _P, _P, c_uint, _P]),
     "nkv_mgs2_step": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
+    "nkv_axpy_dot": (c_int, [_L, _P, _P, _P, _P, _P, _P, _P, c_uint, _P]),
     "nkv_dcgs2_coef_lazy": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, c_int64, _P, _P]),
     "nkv_dcgs2_update_lazy": (c_int, [_L, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_rotate": (c_int, [_L, _P, c_int, _P, c_int, _P]),

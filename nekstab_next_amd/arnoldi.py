@@ -140,14 +140,20 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
             tm.end("block_update", b_upd + 8.0 * lay.n_v)
         ctx.comm.allreduce_(nrm)
     elif mode == "mgs2":
-        for h in (h1, h2):
+        # the reference's order (:155-186): alpha_0 by a dot, then per column one fused pass
+        # (nkv_axpy_dot: f -= alpha_i q_i and the next coefficient — alpha_{i+1}, the second pass's
+        # alpha_0, or finally ||f||^2 — from the same read of f), each coefficient all-reduced
+        ctx.call("nkv_dot", w, f.ptr, Q.col_ptr(0), h1[0:1].data_ptr(), ws, tf, st)
+        ctx.comm.allreduce_(h1[0:1])
+        fl = NKV_TIME | (NKV_TIME_DOT if tf else 0)
+        for p, h in enumerate((h1, h2)):
             for i in range(j):
-                qi = Q.col_ptr(i)
-                ctx.call("nkv_dot", w, f.ptr, qi, h[i:i + 1].data_ptr(), ws, tf, st)
-                ctx.comm.allreduce_(h[i:i + 1])
-                ctx.call("nkv_axpy_dev", f.ptr, h[i:i + 1].data_ptr(), -1.0, qi, NKV_TIME, st)
-        ctx.call("nkv_dot", w, f.ptr, f.ptr, nrm.data_ptr(), ws, tf, st)
-        ctx.comm.allreduce_(nrm)
+                last = i + 1 == j
+                qn = Q.col_ptr(i + 1) if not last else (Q.col_ptr(0) if p == 0 else None)
+                out = h[i + 1:i + 2] if not last else (h2[0:1] if p == 0 else nrm)
+                ctx.call("nkv_axpy_dot", w, f.ptr, h[i:i + 1].data_ptr(), Q.col_ptr(i), qn, out.data_ptr(), ws, fl,
+                         st)
+                ctx.comm.allreduce_(out)
     else:
         raise ValueError(f"unknown orthogonalisation mode {mode!r}")
     if ctx.timer:

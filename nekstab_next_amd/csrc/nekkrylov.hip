@@ -76,6 +76,9 @@ namespace {
 #ifndef NKV_UPD_ROUNDS
 #define NKV_UPD_ROUNDS 2  // block update (CGS2 passes, DCGS2 close): row-band launches of this many rounds
 #endif                    // (+2 % on update+norm at N=1e8, profiles/r02bh_tune_upd_bands.log)
+#ifndef NKV_AXD_ROUNDS
+#define NKV_AXD_ROUNDS 0  // fused MGS column step (nkv_axpy_dot): row-band launches of this many rounds
+#endif
 #ifndef NKV_FUSE_ROUNDS
 #define NKV_FUSE_ROUNDS 0  // fused CGS2 middle pass: row-band launches of this many rounds (0: one launch)
 #endif
@@ -445,6 +448,53 @@ __global__ __launch_bounds__(kThreads) void k_block_update(const double* __restr
         nrm = block_sum(nrm, lds4);
         if (threadIdx.x == 0) partials[blockIdx.x] = acc_part ? partials[blockIdx.x] + nrm : nrm;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused MGS column step (the reference's order, one pass instead of an axpy and a dot):
+//   f <- f - alpha qa   (all stored rows; NKV_TIME: the time slot too)
+//   partials[b] = sum over this block's weighted rows of w f_new qb   (qb = nullptr: w f_new f_new)
+// The next column's projection coefficient (or, after the last column, the next pass's first one
+// or ||f||^2) comes out of the same read of f.
+// ------------------------------------------------------------------------------------------
+template <int kPairs>
+__global__ __launch_bounds__(kThreads) void k_axpy_dot(const double* __restrict__ qa,
+                                                       const double* __restrict__ alpha,
+                                                       double* __restrict__ f,
+                                                       const double* __restrict__ qb,
+                                                       const double* __restrict__ w, int64_t sv,
+                                                       int tiles_per_field, int tiles_w, int tiles_total,
+                                                       int64_t time_off, int do_time,
+                                                       double* __restrict__ partials, int t_lo, int acc_part) {
+    constexpr int kTile = kThreads * kPairs * 2;
+    __shared__ double lds4[4];
+    const double a = -alpha[0];
+    if (do_time && blockIdx.x == 0 && threadIdx.x == 0) f[time_off] = fma(a, qa[time_off], f[time_off]);
+    double s = 0.0;
+    for (int t = t_lo + blockIdx.x; t < tiles_total; t += gridDim.x) {
+        const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+        double2 fn[kPairs];
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+            const double2 fv = ld2(f + r0 + k * 2 * kThreads);
+            const double2 qv = ldq(qa + r0 + k * 2 * kThreads);
+            fn[k] = make_double2(fma(a, qv.x, fv.x), fma(a, qv.y, fv.y));
+        }
+        if (t < tiles_w) {
+            const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
+#pragma unroll
+            for (int k = 0; k < kPairs; ++k) {
+                const double2 wv = ld2(w + wr + k * 2 * kThreads);
+                const double2 bv = qb ? ldq(qb + r0 + k * 2 * kThreads) : fn[k];
+                s = fma(wv.x * fn[k].x, bv.x, s);
+                s = fma(wv.y * fn[k].y, bv.y, s);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) st2(f + r0 + k * 2 * kThreads, fn[k]);
+    }
+    s = block_sum(s, lds4);   // a row band after the first adds to the block's partial (fixed order)
+    if (threadIdx.x == 0) partials[blockIdx.x] = acc_part ? partials[blockIdx.x] + s : s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2229,17 +2279,21 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
         return nkv_arnoldi_finish(L, f, nrm, q_out, 0, h1, nullptr, hcol_dev, 0, stream);
     }
     if (flags & NKV_MGS2) {   // :155-186 in the reference's order; H(i,k) = alpha1 + alpha2 in finish
+        // alpha_0 by a dot, then per column ONE fused pass: f -= alpha_i q_i and the next coefficient
+        // (alpha_{i+1}, the second pass's alpha_0, or finally ||f||^2) from the same read of f
+        CHECK(nkv_dot(L, w, f, Q, h1, ws, tf, stream));
+        CHECK(reduce(h1, 1, "first MGS pass"));
         for (int pass = 0; pass < 2; ++pass) {
             double* h = pass == 0 ? h1 : h2;
             for (int i = 0; i < j; ++i) {
                 const double* qi = Q + (int64_t)i * L->ld;
-                CHECK(nkv_dot(L, w, f, qi, h + i, ws, tf, stream));
-                CHECK(reduce(h + i, 1, pass == 0 ? "first MGS pass" : "second MGS pass"));
-                CHECK(nkv_axpy_dev(L, f, h + i, -1.0, qi, NKV_TIME, stream));
+                const bool last = i + 1 == j;
+                const double* qn = !last ? qi + L->ld : (pass == 0 ? Q : nullptr);   // nullptr: ||f||^2
+                double* out = !last ? h + i + 1 : (pass == 0 ? h2 : nrm);
+                CHECK(nkv_axpy_dot(L, w, f, h + i, qi, qn, out, ws, NKV_TIME | (tf ? NKV_TIME_DOT : 0u), stream));
+                CHECK(reduce(out, 1, last ? (pass == 0 ? "second MGS pass" : "norm") : (pass == 0 ? "first MGS pass" : "second MGS pass")));
             }
         }
-        CHECK(nkv_dot(L, w, f, f, nrm, ws, tf, stream));
-        CHECK(reduce(nrm, 1, "norm"));
         return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
     }
     CHECK(nkv_block_dot(L, w, Q, j, f, h1, ws, tf, stream));
@@ -2315,6 +2369,46 @@ __global__ void k_accumulate(double* __restrict__ dst, const double* __restrict_
     if (threadIdx.x == 0) dst[0] += src[0];
 }
 
+int nkv_axpy_dot(const nkv_layout* L, const double* w, double* f, const double* alpha_dev, const double* qa,
+                 const double* qb, double* out_dev, void* ws, unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(qa, "qa"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!alpha_dev || !out_dev) return fail(NKV_EINVAL, "alpha_dev/out_dev is NULL");
+    if (qb) CHECK(check_ptr(qb, "qb"));
+    const int P = use_large_tiles(L) ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    const int kTile = kThreads * P * 2;
+    const int tpf = (int)(L->sv / kTile);
+    const int tiles_w = tpf * L->n_wf;
+    const int tiles_total = (int)(rows_of(L) / kTile);
+    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    if (g < 1) g = 1;
+    const int64_t T = rows_of(L);
+    const int dt = (flags & NKV_TIME) ? 1 : 0;
+    double* part = partials_of(ws);
+    hipStream_t st = S(stream);
+    auto kern = P == NKV_PAIRS ? k_axpy_dot<NKV_PAIRS> : k_axpy_dot<NKV_PAIRS_SMALL>;
+    // NKV_AXD_ROUNDS > 0: one launch per row band of that many grid-stride rounds (first band: whole grid)
+    const int64_t b = (int64_t)NKV_AXD_ROUNDS * g;
+    const int band = (NKV_AXD_ROUNDS <= 0 || b >= tiles_total || tiles_total < 2 * b) ? (tiles_total > 0 ? tiles_total : 1)
+                                                                                        : (int)b;
+    for (int lo = 0; lo == 0 || lo < tiles_total; lo += band) {
+        const int hi = lo + band < tiles_total ? lo + band : tiles_total;
+        const int gb = lo == 0 ? g : (g < hi - lo ? g : hi - lo);
+        hipLaunchKernelGGL(kern, dim3(gb), dim3(kThreads), 0, st, qa, alpha_dev, f, qb, w, L->sv, tpf, tiles_w, hi, T,
+                           lo == 0 ? dt : 0, part, lo, lo == 0 ? 0 : 1);
+        NKV_LAUNCHED();
+    }
+    const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;   // the replicated time product, once
+    const double* tq = qb ? qb : f;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, tiles_total > 0 ? g : 0, out_dev,
+                       tdot ? tq + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
 int nkv_mgs2_step(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
                   double* hcol_dev, void* ws, unsigned flags, void* stream) {
     CHECK(check_layout(L));
@@ -2328,19 +2422,25 @@ int nkv_mgs2_step(const nkv_layout* L, const double* w, const double* Q, int j, 
     const unsigned tdot = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
     double* tmp = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 128);   // control-area scratch
     hipStream_t st = S(stream);
-    for (int pass = 0; pass < 2; ++pass) {   // krylov_decomposition.f90:155-168, then :171-180
+    // krylov_decomposition.f90:155-168, then :171-180: alpha_0 by a dot, then per column one fused
+    // pass (f -= alpha_i q_i, next coefficient from the same read; the second pass's alphas
+    // alternate between tmp[0] and tmp[2], ||f||^2 lands in tmp[1])
+    if (j > 0) CHECK(nkv_dot(L, w, f, Q, hcol_dev, ws, tdot, st));
+    for (int pass = 0; pass < 2; ++pass) {
         for (int i = 0; i < j; ++i) {
             const double* qi = Q + (int64_t)i * L->ld;
-            double* h = pass == 0 ? hcol_dev + i : tmp;
-            CHECK(nkv_dot(L, w, f, qi, h, ws, tdot, st));                   // alpha = <f, q_i>
-            CHECK(nkv_axpy_dev(L, f, h, -1.0, qi, NKV_TIME, st));           // f <- f - alpha q_i
+            double* h = pass == 0 ? hcol_dev + i : tmp + 2 * (i & 1);
+            const bool last = i + 1 == j;
+            const double* qn = !last ? qi + L->ld : (pass == 0 ? Q : nullptr);
+            double* out = !last ? (pass == 0 ? hcol_dev + i + 1 : tmp + 2 * ((i + 1) & 1)) : (pass == 0 ? tmp : tmp + 1);
             if (pass == 1) {
-                hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, st, hcol_dev + i, tmp);   // H(i,k) += alpha2
+                hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, st, hcol_dev + i, h);   // H(i,k) += alpha2
                 NKV_LAUNCHED();
             }
+            CHECK(nkv_axpy_dot(L, w, f, h, qi, qn, out, ws, NKV_TIME | (tdot ? NKV_TIME_DOT : 0u), st));
         }
     }
-    CHECK(nkv_dot(L, w, f, f, tmp + 1, ws, tdot, st));                       // ||f||^2
+    if (j == 0) CHECK(nkv_dot(L, w, f, f, tmp + 1, ws, tdot, st));          // ||f||^2
     const int64_t rows = rows_of(L);                                          // q_out = f/||f||, H(k+1,k)
     hipLaunchKernelGGL(k_finish, dim3(grid_for(rows / 2)), dim3(kThreads), 0, st, f, tmp + 1, q_out, rows, rows, 0,
                        nullptr, nullptr, nullptr, hcol_dev + j);

@@ -56,6 +56,9 @@ VARIANTS = {
     "upd_r2": {"NKV_UPD_ROUNDS": 2},
     "upd_r4": {"NKV_UPD_ROUNDS": 4},
     "upd_r0": {"NKV_UPD_ROUNDS": 0},   # the single-launch update before r02bh
+    "axd_r1": {"NKV_AXD_ROUNDS": 1},
+    "axd_r2": {"NKV_AXD_ROUNDS": 2},
+    "axd_r4": {"NKV_AXD_ROUNDS": 4},
     "fuse_r1": {"NKV_FUSE_ROUNDS": 1},
     "fuse_r2": {"NKV_FUSE_ROUNDS": 2},
     "fuse_r4": {"NKV_FUSE_ROUNDS": 4},
@@ -226,6 +229,9 @@ def run(names, E, rounds, js, only=None):
             "dcgs2_lazy": (lambda: L.nkv_dcgs2_update_lazy(Lp, Q.data_ptr(), j - 1, coefs[j].data_ptr(), f.data_ptr(),
                                                             f2.data_ptr(), ws.data_ptr(), 0x1, st),
                            8.0 * (j * N + 2 * N)),
+            "axpy_dot": (lambda: L.nkv_axpy_dot(Lp, w.data_ptr(), f2.data_ptr(), nrm1.data_ptr(), Q[0].data_ptr(),
+                                                Q[1].data_ptr(), nrm.data_ptr(), ws.data_ptr(), 0x1, st)
+                         if hasattr(L, "nkv_axpy_dot") else 0, 8.0 * (3 * N + Nw + nv)),
             "finish": (lambda: L.nkv_arnoldi_finish(Lp, f.data_ptr(), nrm1.data_ptr(), f2.data_ptr(), 0, None, None,
                                                     None, 0, st), 16.0 * N),
             "op_diag": (lambda: L.nkv_op_diag(Lp, dgl.data_ptr(), f.data_ptr(), f2.data_ptr(), 0.0, st), 24.0 * N),
