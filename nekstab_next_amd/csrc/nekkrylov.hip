@@ -2378,7 +2378,9 @@ int nkv_axpy_dot(const nkv_layout* L, const double* w, double* f, const double* 
     CHECK(check_ptr(ws, "ws"));
     if (!alpha_dev || !out_dev) return fail(NKV_EINVAL, "alpha_dev/out_dev is NULL");
     if (qb) CHECK(check_ptr(qb, "qb"));
-    const int P = use_large_tiles(L) ? NKV_PAIRS : NKV_PAIRS_SMALL;
+    // 4 double2 per thread at every size: +5 % over the 8 of the wide kernels at N=1e8 for this
+    // four-stream shape (profiles/r02bl_tune_fewcol.log)
+    constexpr int P = NKV_PAIRS_SMALL;
     const int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
     const int tiles_w = tpf * L->n_wf;
@@ -2389,7 +2391,7 @@ int nkv_axpy_dot(const nkv_layout* L, const double* w, double* f, const double* 
     const int dt = (flags & NKV_TIME) ? 1 : 0;
     double* part = partials_of(ws);
     hipStream_t st = S(stream);
-    auto kern = P == NKV_PAIRS ? k_axpy_dot<NKV_PAIRS> : k_axpy_dot<NKV_PAIRS_SMALL>;
+    auto kern = k_axpy_dot<P>;
     // NKV_AXD_ROUNDS > 0: one launch per row band of that many grid-stride rounds (first band: whole grid)
     const int64_t b = (int64_t)NKV_AXD_ROUNDS * g;
     const int band = (NKV_AXD_ROUNDS <= 0 || b >= tiles_total || tiles_total < 2 * b) ? (tiles_total > 0 ? tiles_total : 1)

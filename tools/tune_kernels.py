@@ -56,6 +56,8 @@ VARIANTS = {
     "upd_r2": {"NKV_UPD_ROUNDS": 2},
     "upd_r4": {"NKV_UPD_ROUNDS": 4},
     "upd_r0": {"NKV_UPD_ROUNDS": 0},   # the single-launch update before r02bh
+    "pairs4": {"NKV_PAIRS": 4},
+    "maxb2048": {"NKV_MAXB": 2048},
     "axd_r1": {"NKV_AXD_ROUNDS": 1},
     "axd_r2": {"NKV_AXD_ROUNDS": 2},
     "axd_r4": {"NKV_AXD_ROUNDS": 4},
