@@ -79,6 +79,9 @@ namespace {
 #ifndef NKV_AXD_ROUNDS
 #define NKV_AXD_ROUNDS 0  // fused MGS column step (nkv_axpy_dot): row-band launches of this many rounds
 #endif
+#ifndef NKV_FUSE_SMALL_J
+#define NKV_FUSE_SMALL_J 12  // fused CGS2 middle pass: 4-wave workgroups up to this many columns
+#endif                       // (profiles/r02bn_tune_fuse_small*.log); 0 disables
 #ifndef NKV_FUSE_ROUNDS
 #define NKV_FUSE_ROUNDS 0  // fused CGS2 middle pass: row-band launches of this many rounds (0: one launch)
 #endif
@@ -1974,7 +1977,14 @@ int nkv_block_update_dot(const nkv_layout* L, const double* w, const double* Q, 
     }
     constexpr int NW = NKV_FUSE_NW;
     const int cpw = j <= NW * 16 ? (j + NW - 1) / NW : (j + 15) / 16;
-    if (j <= NW * 16) {
+    if (j <= NKV_FUSE_SMALL_J) {   // few columns: 4 waves per workgroup (+4 % at j = 8, +28 % at j = 2)
+        switch ((j + 3) / 4) {
+            case 1: NKV_FUSE(4, 1); break;
+            case 2: NKV_FUSE(4, 2); break;
+            case 3: NKV_FUSE(4, 3); break;
+            default: NKV_FUSE(4, 4); break;
+        }
+    } else if (j <= NW * 16) {
         switch (cpw) {
             case 1: NKV_FUSE(NW, 1); break;
             case 2: NKV_FUSE(NW, 2); break;
