@@ -79,6 +79,10 @@ namespace {
 #ifndef NKV_AXD_ROUNDS
 #define NKV_AXD_ROUNDS 0  // fused MGS column step (nkv_axpy_dot): row-band launches of this many rounds
 #endif
+#ifndef NKV_UPD_SMALL_J
+#define NKV_UPD_SMALL_J 2   // block update: 4x the workgroups up to this many columns (+5-9 % at j <= 2,
+                            // neutral to -4 % from j = 4 on: profiles/r02br_tune_upd_small*.log)
+#endif
 #ifndef NKV_FUSE_SMALL_J
 #define NKV_FUSE_SMALL_J 12  // fused CGS2 middle pass: 4-wave workgroups up to this many columns
 #endif                       // (profiles/r02bn_tune_fuse_small*.log); 0 disables
@@ -1755,7 +1759,10 @@ int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q,
     const int tpf = (int)(L->sv / kTile);
     const int tiles_w = tpf * L->n_wf;
     const int tiles_total = (int)(rows_of(L) / kTile);
-    int g = tiles_total < kMaxBlocks ? tiles_total : kMaxBlocks;
+    // few columns: a 4x larger grid (the norm partials still fit: the workspace holds at least
+    // 4 * kMaxBlocks slots, nkv_workspace_bytes with max_cols >= 1)
+    const int gmax = j <= NKV_UPD_SMALL_J ? 4 * kMaxBlocks : kMaxBlocks;
+    int g = tiles_total < gmax ? tiles_total : gmax;
     if (g < 1) g = 1;
     *g_out = g;
     const int64_t T = rows_of(L);

@@ -60,7 +60,9 @@ VARIANTS = {
     "fg512": {"NKV_FUSE_G": 512},
     "fg2048": {"NKV_FUSE_G": 2048},
     "fnw4": {"NKV_FUSE_NW": 4},
-    "fsmall0": {"NKV_FUSE_SMALL_J": 0},   # the fused pass before r02bn (8 waves at every small j)
+    "fsmall0": {"NKV_FUSE_SMALL_J": 0},
+    "usmall4": {"NKV_UPD_SMALL_J": 4},
+    "usmall8": {"NKV_UPD_SMALL_J": 8},   # the fused pass before r02bn (8 waves at every small j)
     "maxb2048": {"NKV_MAXB": 2048},
     "axd_r1": {"NKV_AXD_ROUNDS": 1},
     "axd_r2": {"NKV_AXD_ROUNDS": 2},
