@@ -49,6 +49,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 spec (vector = matrix on CDNA4); SURVEY.md §8(d) ridge ~10 flop/B
 N_HEADLINE = 100_014_464  # config 3, E=44,176
+# multi-rank wall clocks (seconds; env NKV_RANK_WALL_S / NKV_LAUNCH_WALL_S override, <= 0 disables):
+# a rank ends itself first (stack dump, status 124), the launcher is the backstop; both sit below the
+# driver's 600 s budget for one bench line
+DEFAULT_RANK_WALL_S = "540"
+DEFAULT_LAUNCH_WALL_S = "570"
 
 
 # ---- byte models ---------------------------------------------------------------------------------
@@ -225,10 +230,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch(n: int, argv, grace_s: float = 60.0) -> int:
+def launch(n: int, argv, grace_s: float = 60.0, wall_s: float = 0.0) -> int:
     """Spawn ``n`` ranks of this script (torch.distributed.run's environment, no exec) and return
     the worst exit status.  If one rank fails, the others get ``grace_s`` to finish (a rank blocked
-    in a collective never does) and are then terminated."""
+    in a collective never does) and are then terminated.  ``wall_s`` > 0 bounds the whole job: a
+    hang in which every rank sits in a collective (no rank exits, so no grace period starts) is
+    terminated at ``wall_s`` and the launcher exits 124 — before the driver's own limit."""
     port = int(os.environ.get("MASTER_PORT") or _free_port())
     procs = []
     for r in range(n):
@@ -245,8 +252,17 @@ def launch(n: int, argv, grace_s: float = 60.0) -> int:
     old = {s: signal.signal(s, _stop) for s in (signal.SIGTERM, signal.SIGINT)}
     rcs = [None] * n
     t_fail = None
+    t_start = time.monotonic()
+    timed_out = False
     try:
         while any(rc is None for rc in rcs):
+            if wall_s > 0 and not timed_out and time.monotonic() - t_start > wall_s:
+                timed_out = True
+                alive = [i for i in range(n) if rcs[i] is None]
+                print(f"bench launcher: wall clock of {wall_s:.0f} s exceeded with ranks {alive} still running; "
+                      "terminating every rank", file=sys.stderr, flush=True)
+                t_fail = time.monotonic() - grace_s - 1.0     # no grace: stop them now
+
             for i, p in enumerate(procs):
                 if rcs[i] is None:
                     rc = p.poll()
@@ -271,7 +287,8 @@ def launch(n: int, argv, grace_s: float = 60.0) -> int:
         for s, h in old.items():
             signal.signal(s, h)
     norm = [rc if rc >= 0 else 128 - rc for rc in rcs]   # killed by signal k -> 128 + k
-    return max(norm)
+    worst = max(norm)
+    return 124 if timed_out and worst in (0, 128 + signal.SIGTERM, 128 + signal.SIGKILL) else worst
 
 
 def parse_args(argv=None):
@@ -296,6 +313,9 @@ def parse_args(argv=None):
                     help="at one GPU, route every partial through a world-1 RCCL group (collective cost)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print each rank's launch environment and stop before GPU initialisation")
+    ap.add_argument("--collective-probe", action="store_true",
+                    help="CPU test of the collective path: init the process group (bounded timeout, rank "
+                         "watchdog), gather the ranks' device identities, one all-reduce, print one JSON line")
     return ap.parse_args(argv)
 
 
@@ -303,7 +323,8 @@ def main():
     args = parse_args()
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
-        sys.exit(launch(args.gpus, sys.argv[1:], grace_s=float(os.environ.get("NKV_LAUNCH_GRACE_S", "60"))))
+        sys.exit(launch(args.gpus, sys.argv[1:], grace_s=float(os.environ.get("NKV_LAUNCH_GRACE_S", "60")),
+                        wall_s=float(os.environ.get("NKV_LAUNCH_WALL_S", DEFAULT_LAUNCH_WALL_S))))
     world_env = int(ws) if ws is not None else 1
     if world_env != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; refusing to run", file=sys.stderr)
@@ -315,6 +336,15 @@ def main():
         r = os.environ.get("RANK", "0")   # test hooks: a rank that hangs / fails
         time.sleep(float(os.environ.get("NKV_DRY_SLEEP_RANK" + r, "0")))
         sys.exit(int(os.environ.get("NKV_DRY_RC_RANK" + r, "0")))
+    if world_env > 1:
+        # last-resort per-rank wall clock (also under torch.distributed.run, where no launcher of
+        # ours is the parent): ends a rank stuck past NKV_RANK_WALL_S with status 124
+        from nekstab_next_amd.comm import start_rank_watchdog
+
+        start_rank_watchdog(float(os.environ.get("NKV_RANK_WALL_S", DEFAULT_RANK_WALL_S)),
+                            label=f"bench.py rank {os.environ.get('RANK', '?')}")
+    if args.collective_probe:
+        sys.exit(collective_probe())
     # the contract's ONE JSON line: keep the real stdout for it and send everything else that
     # writes to fd 1 (gloo's C++ connection banner, library prints) to stderr
     sys.stdout.flush()
@@ -324,6 +354,44 @@ def main():
 
 
 # ---- one rank ----------------------------------------------------------------------------------
+
+def collective_probe() -> int:
+    """``--collective-probe``: the multi-rank plumbing without the solver (CPU tests: gloo ranks).
+    Process-group init with the bounded timeout, the ranks' device identities, one SUM all-reduce;
+    ``NKV_PROBE_HANG_RANK=r`` makes rank r never join the all-reduce, so its peers' collective
+    times out (NKV_COLLECTIVE_TIMEOUT_S) and every rank must end non-zero within the bounds."""
+    import torch
+
+    from nekstab_next_amd.comm import init_from_env
+
+    comm = init_from_env(os.environ.get("NKV_BACKEND", "gloo"))
+    devs = comm.devices()
+    hang = os.environ.get("NKV_PROBE_HANG_RANK")
+    if hang is not None and int(hang) == comm.rank:
+        print(f"probe rank {comm.rank}: not joining the all-reduce", file=sys.stderr, flush=True)
+        time.sleep(3600)
+    t = torch.tensor([float(comm.rank + 1)], dtype=torch.float64)
+    t0 = time.monotonic()
+    try:
+        comm.allreduce_(t)
+    except Exception as e:  # noqa: BLE001 - the bounded collective's timeout, reported and fatal
+        print(f"probe rank {comm.rank}: all-reduce failed after {time.monotonic() - t0:.1f} s: "
+              f"{type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}", file=sys.stderr, flush=True)
+        return 3
+    if comm.rank == 0:
+        print(json.dumps({"collective_probe": True, "world": comm.world, "backend": comm.backend,
+                          "sum": float(t.item()), "devices": devs,
+                          "distinct_devices": distinct_devices(devs)}), flush=True)
+    return 0
+
+
+def distinct_devices(devs) -> bool | None:
+    """True iff every rank drove a different GPU (PCI address + host); None without GPUs."""
+    keys = [(d.get("host"), d.get("pci")) for d in devs]
+    if any(k[1] is None for k in keys):
+        return None
+    return len(set(keys)) == len(keys)
+
 
 def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed):
     """BASELINE config 3's Krylov–Schur leg at full N with restarts that really happen: the
@@ -379,6 +447,7 @@ def run(args):
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    devices = comm.devices(dev)      # per-rank GPU identity (gathered at world > 1)
 
     glay = box3d_layout(args.E)
     lay = glay.shard(rank, world)
@@ -550,6 +619,8 @@ def run(args):
             "n_gpus": world,
             "world": world,
             "backend": comm.backend if world > 1 or args.force_collectives else None,
+            "devices": devices,
+            "distinct_devices": distinct_devices(devices),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),

@@ -231,7 +231,8 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
  * only normalises.  scratch_dev: nkv_arnoldi_scratch_doubles(j) doubles; ws: nkv_workspace_bytes(L, j)
  * bytes at least.  flags: NKV_TIME_DOT
  * (time products in the dots); NKV_MGS2: the reference's own order instead (:155-186, two MGS passes,
- * one dot + all-reduce + axpy per column; j+3 scratch doubles).  For per-column consumers (GMRES: newton_krylov.f90:252) and
+ * one dot + all-reduce + axpy per column; 2j+3 scratch doubles, covered by nkv_arnoldi_scratch_doubles(j)).
+ * For per-column consumers (GMRES: newton_krylov.f90:252) and
  * checkpointing Arnoldi, where each column must be final when its step returns. */
 int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q, int j, double* f, double* q_out,
                           double* hcol_dev, double* scratch_dev, void* ws, nkv_allreduce_fn allreduce, void* ar_user,

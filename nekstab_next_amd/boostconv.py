@@ -23,6 +23,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import _lib
 from .layout import NekLayout
 from .vector import NekContext, NekVector
 
@@ -90,6 +91,12 @@ class BoostConv:
             ctx.call("nkv_normalize_dev", dum.ptr, nrm[j:j + 1].data_ptr(), D[j * n + j:].data_ptr(), 0, st)
             self.Q[j].copy_from(dum, time=False)
         if bool((nrm[1:] < 1e-60).any()):   # the only host synchronisation of the QR
+            # the device normalised the zero column (0 * inf = NaN) and the later dots against it
+            # raised the workspace NaN flag: clear it, the host form below recomputes every scalar
+            # (and its own dots still flag a NaN that is really in Y)
+            code = ctx.lib.nkv_check_status(ctx.ws.data_ptr(), ctx.stream)
+            if code not in (_lib.NKV_OK, _lib.NKV_ENAN):
+                _lib.check(code, "nkv_check_status")
             return False
         self.dd = D.view(n, n).cpu().numpy()
         if np.isnan(self.dd).any():

@@ -8,10 +8,59 @@ length j in device memory and a single all-reduce of that vector (RCCL over xGMI
 """
 from __future__ import annotations
 
+import datetime
+import faulthandler
 import os
+import sys
+import threading
 
 import torch
 import torch.distributed as dist
+
+# A collective that does not complete within this bound aborts the rank with a message instead of
+# blocking it for torch's default 10 min (longer than the bench budget).  RCCL: the watchdog thread
+# of ProcessGroupNCCL enforces it (async error handling on); gloo: every collective honours it.
+DEFAULT_COLLECTIVE_TIMEOUT_S = 120.0
+
+
+def collective_timeout_s() -> float:
+    return float(os.environ.get("NKV_COLLECTIVE_TIMEOUT_S", DEFAULT_COLLECTIVE_TIMEOUT_S))
+
+
+def start_rank_watchdog(seconds: float | None = None, label: str = "rank"):
+    """Last-resort wall clock for one rank: after ``seconds`` (``NKV_RANK_WALL_S``; unset or <= 0:
+    none) dump every thread's stack to stderr and end the process with status 124 — a hang that
+    no collective timeout catches (every rank blocked in a collective, under torch.distributed.run
+    where bench.py's own launcher is not the parent) still ends before the driver's limit.  Ends
+    the process, never execs (no program replacement after GPU initialisation)."""
+    if seconds is None:
+        seconds = float(os.environ.get("NKV_RANK_WALL_S", "0") or 0)
+    if seconds <= 0:
+        return None
+
+    def _fire():
+        print(f"{label}: wall clock of {seconds:.0f} s exceeded; aborting this rank (status 124)",
+              file=sys.stderr, flush=True)
+        try:
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        finally:
+            os._exit(124)
+
+    t = threading.Timer(seconds, _fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def device_identity(device=None) -> dict:
+    """This rank's GPU: index, name, PCI domain:bus:device and UUID (None on a CPU-only rank)."""
+    if not torch.cuda.is_available():
+        return {"device": None, "name": "cpu", "pci": None, "uuid": None, "host": os.uname().nodename}
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index
+    pr = torch.cuda.get_device_properties(idx)
+    pci = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    return {"device": int(idx), "name": pr.name, "pci": pci, "uuid": str(getattr(pr, "uuid", "")),
+            "host": os.uname().nodename}
 
 
 class Comm:
@@ -46,6 +95,15 @@ class Comm:
                 tm.end("allreduce", 8.0 * t.numel())
         return t
 
+    def devices(self, device=None) -> list:
+        """Every rank's :func:`device_identity`, in rank order (a collective at world > 1)."""
+        me = device_identity(device)
+        if self.world == 1:
+            return [me]
+        out = [None] * self.world
+        dist.all_gather_object(out, me, group=self.group)
+        return out
+
     def barrier(self) -> None:
         if self.world > 1:
             dist.barrier(group=self.group)
@@ -66,6 +124,9 @@ def init_from_env(backend: str | None = None, force_collectives: bool = False) -
     ``force_collectives`` at world size 1: initialise a world-1 group anyway and route every
     partial through it (the cost of the collective path without peers)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # bounded collectives: set before the process group exists (RCCL reads it at creation)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    tmo = datetime.timedelta(seconds=collective_timeout_s())
     if world == 1 and force_collectives and not dist.is_initialized():
         import socket
 
@@ -78,7 +139,8 @@ def init_from_env(backend: str | None = None, force_collectives: bool = False) -
         if backend == "nccl":
             torch.cuda.set_device(0)
             kw["device_id"] = torch.device("cuda", 0)
-        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **kw)
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                timeout=tmo, **kw)
         return Comm(force_collectives=True)
     if world > 1 and not dist.is_initialized():
         if backend is None:
@@ -87,9 +149,9 @@ def init_from_env(backend: str | None = None, force_collectives: bool = False) -
         if backend == "nccl":
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", local), timeout=tmo)
         else:  # gloo: CPU tests, or several ranks sharing one GPU (rehearsal of the sharded path)
             if torch.cuda.is_available():
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     return Comm()

@@ -86,6 +86,8 @@ namespace {
 #ifndef NKV_FUSE_SMALL_J
 #define NKV_FUSE_SMALL_J 12  // fused CGS2 middle pass: 4-wave workgroups up to this many columns
 #endif                       // (profiles/r02bn_tune_fuse_small*.log); 0 disables
+static_assert(NKV_FUSE_SMALL_J >= 0 && NKV_FUSE_SMALL_J <= 16,
+              "the 4-wave fused pass instantiates at most 16 columns (NKV_FUSE(4, 4))");
 #ifndef NKV_FUSE_ROUNDS
 #define NKV_FUSE_ROUNDS 0  // fused CGS2 middle pass: row-band launches of this many rounds (0: one launch)
 #endif
@@ -2281,6 +2283,11 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
     CHECK(check_layout(L));
     if (!hcol_dev || !scratch_dev) return fail(NKV_EINVAL, "hcol/scratch is NULL");
     if (j < 0 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "j=%d outside 0..%d", j, NKV_MAX_COLS);
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(q_out, "q_out"));
+    CHECK(check_ptr(ws, "ws"));
+    if (j > 0) CHECK(check_ptr(Q, "Q"));
     const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
     double* h1 = scratch_dev;
     double* h2 = scratch_dev + (j + 1);

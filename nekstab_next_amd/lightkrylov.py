@@ -127,8 +127,12 @@ def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, toler
             nan = False
         except NkvNaNError:
             nan = True
-        if not (nan or breakdown_column(Cd.download(), 0, k, breakdown_tol, offset=0) >= 0
-                or breakdown_column(Dd.download(), 0, k, breakdown_tol, offset=1) >= 0):
+        broken_here = (nan or breakdown_column(Cd.download(), 0, k, breakdown_tol, offset=0) >= 0
+                       or breakdown_column(Dd.download(), 0, k, breakdown_tol, offset=1) >= 0)
+        if ctx.comm.world > 1:   # the C/D tests are replicated; the NaN flag is per rank
+            flag = torch.tensor([1.0 if broken_here else 0.0], dtype=torch.float64, device=ctx.device)
+            broken_here = float(ctx.comm.allreduce_(flag).item()) > 0.0
+        if not broken_here:
             break
         mode, broken = _mgs2_of(mode), True
     Ct = Cd.download()  # (k+1, k): column j-1 holds <u_i, A v_j> (i < j) and alpha_j at row j-1

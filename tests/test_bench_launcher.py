@@ -70,3 +70,54 @@ def test_single_gpu_default_runs_in_process():
     assert p.returncode == 0
     recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(recs) == 1 and recs[0]["WORLD_SIZE"] is None
+
+
+# ---- round 3: bounded collectives, wall clocks, per-rank device identity ----
+
+def test_collective_probe_gathers_devices():
+    p = _run(["--gpus", "2", "--collective-probe"], _env(NKV_BACKEND="gloo"), timeout=120)
+    assert p.returncode == 0, p.stderr
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["world"] == 2 and rec["backend"] == "gloo" and rec["sum"] == 3.0
+    assert len(rec["devices"]) == 2
+    # CPU ranks have no GPU identity: distinct_devices is undecidable, not true
+    assert rec["distinct_devices"] is None
+
+
+def test_rank_missing_from_allreduce_ends_every_rank():
+    """One rank never joins the all-reduce: its peer's collective times out (bounded by
+    NKV_COLLECTIVE_TIMEOUT_S instead of torch's 10 min), that rank exits non-zero, and the
+    launcher ends the absent rank and exits non-zero — all within the bound."""
+    t0 = time.monotonic()
+    p = _run(["--gpus", "2", "--collective-probe"],
+             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="4",
+                  NKV_LAUNCH_GRACE_S="2", NKV_RANK_WALL_S="0"), timeout=120)
+    dt = time.monotonic() - t0
+    assert dt < 60, dt
+    assert p.returncode != 0
+    assert "probe rank 0: all-reduce failed" in p.stderr, p.stderr[-2000:]
+    assert "bench launcher: rank 0 exited with 3" in p.stderr
+
+
+def test_rank_watchdog_ends_a_hung_rank():
+    """Under torch.distributed.run (no launcher of ours): the per-rank wall clock alone ends a rank
+    that never returns, with status 124 and a stack dump."""
+    t0 = time.monotonic()
+    p = _run(["--gpus", "2", "--collective-probe"],
+             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="600",
+                  NKV_LAUNCH_GRACE_S="600", NKV_RANK_WALL_S="6", NKV_LAUNCH_WALL_S="0"), timeout=120)
+    assert time.monotonic() - t0 < 60
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    assert "wall clock of 6 s exceeded" in p.stderr
+
+
+def test_launcher_wall_clock_ends_an_all_ranks_hang():
+    """Every rank blocked (no rank exits, so no grace period starts): the launcher's wall clock
+    terminates them all and exits 124."""
+    t0 = time.monotonic()
+    p = _run(["--gpus", "3", "--dry-launch"],
+             _env(NKV_DRY_SLEEP_RANK0="300", NKV_DRY_SLEEP_RANK1="300", NKV_DRY_SLEEP_RANK2="300",
+                  NKV_LAUNCH_WALL_S="3", NKV_RANK_WALL_S="0"), timeout=120)
+    assert time.monotonic() - t0 < 40
+    assert p.returncode == 124, p.returncode
+    assert "wall clock of 3 s exceeded" in p.stderr

@@ -343,6 +343,13 @@ def test_native_dcgs2_driver_callback_errors(gpu):
     rc = ctx.lib.nkv_update_hessenberg(ctx._Lp, ctx.w.data_ptr(), Q.ptr, -1, f.ptr, Q.col_ptr(1), Hd.t.data_ptr(),
                                        scratch.data_ptr(), ctx.ws.data_ptr(), L_.ALLREDUCE_FN(), None, 0, ctx.stream)
     assert rc == L_.NKV_EINVAL
+    # NULL operands are refused before any launch
+    for i, what in ((1, "w"), (4, "f"), (5, "q_out"), (8, "ws"), (2, "Q")):
+        a = [ctx._Lp, ctx.w.data_ptr(), Q.ptr, 2, f.ptr, Q.col_ptr(2), Hd.t.data_ptr(), scratch.data_ptr(),
+             ctx.ws.data_ptr(), L_.ALLREDUCE_FN(), None, 0, ctx.stream]
+        a[i] = None
+        rc = ctx.lib.nkv_update_hessenberg(*a)
+        assert rc == L_.NKV_EINVAL and f"{what} is NULL" in L_.last_error(), (what, L_.last_error())
     # the per-column one-call factorisation: the same argument checks and callback failure
     for args, what in (((1, 4, 4, scratch.data_ptr()), "ldh"), ((0, 4, 5, scratch.data_ptr()), "outside"),
                        ((1, 4, 5, None), "scratch")):
