@@ -309,6 +309,16 @@ int nkv_op_rot2(const nkv_layout* L, const double* c, const double* s, const dou
 int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const double* x, double* y, int conj,
                  void* stream);
 
+/* ---- sensitivity post-processing (sensitivity.f90) ---------------------------------------
+ * wave_maker's pointwise product (sensitivity.f90:69-71), after biorthogonalize (:63-66):
+ *   out[i] = sqrt(sum_c dRe_c[i]^2 + dIm_c[i]^2) * sqrt(sum_c aRe_c[i]^2 + aIm_c[i]^2),
+ * c over the first ncomp (2 or 3, <= n_wf) weighted fields — the velocity components — summed in
+ * the reference's left-to-right order without contraction.  out: sv doubles (one field segment;
+ * padding rows give 0).  The reference's 2-D case adds its uninitialised vz arrays; here ncomp = 2
+ * has no vz terms. */
+int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
+                  double* out, int ncomp, void* stream);
+
 /* ---- shard-independent synthetic data ----------------------------------------------------
  * x[row] = 2*u - 1, u = hash(seed, field, global point) in [0,1) with 53 exact bits, for live
  * rows; padding rows = 0; time = 0.  Global point of local point i in a weighted field is

@@ -105,6 +105,7 @@ _SIGNATURES = {
     "nkv_op_rot2": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
     "nkv_op_cdiag": (c_int, [_L, _P, _P, _P, _P, c_int, _P]),
     "nkv_fill_hash": (c_int, [_L, _P, c_uint64, c_int64, c_int64, _P]),
+    "nkv_wavemaker": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
 }
 
 # Every symbol include/nekkrylov.h declares (tests check the .so exports all of them).

@@ -1659,6 +1659,41 @@ __global__ __launch_bounds__(kThreads) void k_op_cdiag(const double* __restrict_
     if (seg == 0 && blockIdx.x == 0 && threadIdx.x == 0) y[time_off] = 0.0;
 }
 
+// wave_maker's pointwise product (sensitivity.f90:69-71):
+//   out[i] = sqrt(vx_dRe^2 + vx_dIm^2 + vy_dRe^2 + ...) * sqrt(vx_aRe^2 + vx_aIm^2 + ...)
+// over NC velocity components, summed left to right in the reference's order with no contraction
+// (bit-identical to a plain restatement).  Pure HBM streaming: 4 NC reads and one write per point.
+template <int NC>
+__global__ __launch_bounds__(kThreads) void k_wavemaker(const double* __restrict__ dRe, const double* __restrict__ dIm,
+                                                        const double* __restrict__ aRe, const double* __restrict__ aIm,
+                                                        double* __restrict__ out, int64_t sv, int64_t pairs) {
+#pragma clang fp contract(off)
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < pairs; p += (int64_t)gridDim.x * kThreads) {
+        double2 dr[NC], di[NC], ar[NC], ai[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            dr[c] = ldq(dRe + c * sv + 2 * p);
+            di[c] = ldq(dIm + c * sv + 2 * p);
+            ar[c] = ldq(aRe + c * sv + 2 * p);
+            ai[c] = ldq(aIm + c * sv + 2 * p);
+        }
+        double2 sd = make_double2(dr[0].x * dr[0].x + di[0].x * di[0].x, dr[0].y * dr[0].y + di[0].y * di[0].y);
+        double2 sa = make_double2(ar[0].x * ar[0].x + ai[0].x * ai[0].x, ar[0].y * ar[0].y + ai[0].y * ai[0].y);
+#pragma unroll
+        for (int c = 1; c < NC; ++c) {
+            sd.x = sd.x + dr[c].x * dr[c].x;
+            sd.x = sd.x + di[c].x * di[c].x;
+            sd.y = sd.y + dr[c].y * dr[c].y;
+            sd.y = sd.y + di[c].y * di[c].y;
+            sa.x = sa.x + ar[c].x * ar[c].x;
+            sa.x = sa.x + ai[c].x * ai[c].x;
+            sa.y = sa.y + ar[c].y * ar[c].y;
+            sa.y = sa.y + ai[c].y * ai[c].y;
+        }
+        st2s(out + 2 * p, make_double2(sqrt(sd.x) * sqrt(sa.x), sqrt(sd.y) * sqrt(sa.y)));
+    }
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -2744,6 +2779,23 @@ int nkv_fill_hash(const nkv_layout* L, double* x, uint64_t seed, int64_t v_offse
     const int64_t rows = rows_of(L);
     hipLaunchKernelGGL(k_fill_hash, dim3(grid_for(rows)), dim3(kThreads), 0, S(stream), x, seed, L->n_wf,
                        L->n_v, L->sv, L->n_p, rows, rows, v_offset, p_offset);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
+                  double* out, int ncomp, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(dRe, "dRe"));
+    CHECK(check_ptr(dIm, "dIm"));
+    CHECK(check_ptr(aRe, "aRe"));
+    CHECK(check_ptr(aIm, "aIm"));
+    CHECK(check_ptr(out, "out"));
+    if (ncomp < 2 || ncomp > 3 || ncomp > L->n_wf)
+        return fail(NKV_EINVAL, "wavemaker: ncomp=%d must be 2 or 3 and <= n_wf=%d", ncomp, L->n_wf);
+    const int64_t pairs = L->sv / 2;
+    auto kern = ncomp == 3 ? k_wavemaker<3> : k_wavemaker<2>;
+    hipLaunchKernelGGL(kern, dim3(grid_for(pairs)), dim3(kThreads), 0, S(stream), dRe, dIm, aRe, aIm, out, L->sv, pairs);
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -99,11 +99,11 @@ class ShiftedOperator(LinearOperator):
 
 
 class RankTwoPerturbed(LinearOperator):
-    """A x = D x + sigma * (u <v, x>_W + v' <u', x>_W): a diagonal plus a rank-2 non-normal term,
-    so direct and adjoint eigenvectors differ.  The adjoint under W is
-    A^T x = D x + sigma * (v <u, x>_W + u' <v', x>_W)."""
+    """A x = D x + sigma * (u <v, x>_W + v' <u', x>_W): a base operator D (config 5: diagonal) plus
+    a rank-2 non-normal term, so direct and adjoint eigenvectors differ.
+    The adjoint under W is A^T x = D^T x + sigma * (v <u, x>_W + u' <v', x>_W)."""
 
-    def __init__(self, diag_op: DiagOperator, u: NekVector, v: NekVector, u2: NekVector, v2: NekVector,
+    def __init__(self, diag_op: LinearOperator, u: NekVector, v: NekVector, u2: NekVector, v2: NekVector,
                  sigma: float):
         self.d, self.u, self.v, self.u2, self.v2, self.sigma = diag_op, u, v, u2, v2, float(sigma)
 
@@ -115,7 +115,7 @@ class RankTwoPerturbed(LinearOperator):
         y.axpby(1.0, self.v2, self.sigma * b)
 
     def rmatvec(self, x: NekVector, y: NekVector) -> None:
-        self.d.matvec(x, y)
+        self.d.rmatvec(x, y)
         a = x.ctx.dot(self.u, x, time=False)
         b = x.ctx.dot(self.v2, x, time=False)
         y.axpby(1.0, self.v, self.sigma * a)

@@ -1,19 +1,28 @@
-"""Direct/adjoint mode bi-orthogonalisation (the device part of nekStab's sensitivity tools).
+"""Direct/adjoint sensitivity post-processing on the device (nekStab's core/sensitivity.f90).
 
-Reference: ``biorthogonalize`` (core/sensitivity.f90:393-469): normalise the direct mode so that
+``biorthogonalize`` (core/sensitivity.f90:393-469): normalise the direct mode so that
 ||Re||^2 + ||Im||^2 = 1 — with ``opcmult``, i.e. the velocity components only (:429-430) — form
 the complex W-inner product <adjoint, direct> from four real ``inner_product`` calls, and rescale
 the adjoint mode (all fields incl. pressure and scalars; ``time`` untouched) so that it becomes 1.
-The gradient post-processing (wave-maker, base-flow sensitivity) needs Nek5000's gradm1/dsavg and
-is out of scope.
+
+``wave_maker`` (core/sensitivity.f90:3-77, Giannetti & Luchini 2007): load the direct mode
+``dRe/dIm<session>0.f00001`` and the adjoint mode ``aRe/aIm<session>0.f00002`` (velocity only:
+``ifto = ifpo = .false.``, :40), bi-orthogonalise them, form the pointwise product
+|u_d| |u_a| = sqrt(sum_c dRe_c^2 + dIm_c^2) sqrt(sum_c aRe_c^2 + aIm_c^2) (:69-71, one streaming
+kernel, ``nkv_wavemaker``) and write it as the temperature field of ``wm_<session>0.f00001``
+(:73-74).  It needs no derivatives.  The base-flow sensitivity (``bf_sensitivity``, :81-269) does
+— Nek5000's ``gradm1``/``dsavg`` on the spectral-element mesh — and stays out of scope.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
+import torch
 
 from . import _lib
+from .layout import NekLayout
 from .vector import NekContext, NekVector
 
 
@@ -44,3 +53,69 @@ def biorthogonalize(ctx: NekContext, dRe: NekVector, dIm: NekVector, aRe: NekVec
     aIm.axpby(gamma / den, aRe, delta / den)    # (gamma aIm + delta aRe)/den
     aRe.copy_from(wk1, time=False)
     return complex(gamma, delta)
+
+
+def velocity_layout(lay: NekLayout) -> NekLayout:
+    """The vector ``wave_maker`` works on: vx, vy, [vz] only — ``ifto = ifpo = .false.``
+    (sensitivity.f90:40), so the dots (inner_product, eigensolvers.f90:46-53) and the copies and
+    scalings (nopcopy/opcmult, nek_vectors.f90:279-298) skip pressure and temperature."""
+    return NekLayout(lay.ldim, lay.lx1, lay.lx2, lay.nelgv, n_scalars=0, ifpo=False, rank=lay.rank, world=lay.world)
+
+
+def wavemaker_field(ctx: NekContext, dRe: NekVector, dIm: NekVector, aRe: NekVector, aIm: NekVector,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """sensitivity.f90:69-71 on the device: one field segment (``sv`` doubles) holding
+    sqrt(sum_c dRe_c^2 + dIm_c^2) * sqrt(sum_c aRe_c^2 + aIm_c^2) over the velocity components."""
+    lay = ctx.layout
+    if out is None:
+        out = torch.empty(lay.sv, dtype=torch.float64, device=ctx.device)
+    if out.numel() < lay.sv:
+        raise ValueError(f"out holds {out.numel()} doubles, {lay.sv} needed")
+    ctx.call("nkv_wavemaker", dRe.ptr, dIm.ptr, aRe.ptr, aIm.ptr, out.data_ptr(), lay.ldim, ctx.stream)
+    return out
+
+
+def wave_maker(ctx: NekContext, directory: str, session: str = "nek", d_num: int = 1, a_num: int = 2,
+               outdir: str | None = None, coords: dict | None = None) -> dict:
+    """``wave_maker`` (sensitivity.f90:3-77) on a velocity-only context (``velocity_layout``).
+
+    Reads the direct mode ``dRe/dIm<session>0.f<d_num>`` and the adjoint mode
+    ``aRe/aIm<session>0.f<a_num>`` (the reference's file numbers 1 and 2, :43-58; multi-file sets:
+    each rank reads its own elements), bi-orthogonalises them on the device, forms the wave-maker
+    field and writes it as the temperature of ``wm_<session><rank>.f00001`` in ``outdir``
+    (default ``directory``).  As in the reference the header carries the time of the last file
+    loaded (Nek5000's ``load_fld`` sets ``time``), no velocity (``ifvo = .false.``) and no
+    pressure (``ifpo = .false.``); ``coords`` ({"x","y"[,"z"]} per local point) adds an X group.
+    Returns the wave-maker (packed, this rank's points), <adjoint, direct>_W before the rescaling
+    and the file written."""
+    from . import fld
+
+    lay = ctx.layout
+    if lay.n_scalars or lay.n_p or lay.n_wf != lay.ldim:
+        raise ValueError("wave_maker works on a velocity-only context (sensitivity.velocity_layout)")
+    vecs, last = [], None
+    for prefix, num in (("dRe", d_num), ("dIm", d_num), ("aRe", a_num), ("aIm", a_num)):
+        files = fld.read_fld_set(directory, prefix, session, num)
+        last = files[0]
+        v = ctx.vector()
+        v.from_packed(fld.vector_from_fld(lay, files))
+        vecs.append(v)
+    dRe, dIm, aRe, aIm = vecs
+    ip = biorthogonalize(ctx, dRe, dIm, aRe, aIm)
+    wm_dev = wavemaker_field(ctx, dRe, dIm, aRe, aIm)
+    ctx.check_nan()
+    wm = wm_dev[: lay.n_v].cpu().numpy()
+    e0, e1 = lay.elem_range()
+    f = fld.FldFile(lay.lx1, lay.lx1, lay.lx1 if lay.ldim == 3 else 1, lay.nelgv, last.time, last.istep, lay.rank,
+                    lay.world, "", np.arange(e0 + 1, e1 + 1, dtype=np.int32), {})
+    if coords:
+        f.fields.update({k: np.asarray(v).reshape(lay.nelv, lay.pts_v) for k, v in coords.items()})
+        f.rdcode += "X"
+    f.fields["t"] = wm.reshape(lay.nelv, lay.pts_v)
+    f.rdcode += "T"
+    out = outdir or directory
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, fld.fld_name("wm_", session, lay.rank, 1))
+    fld.write_fld(path, f)
+    return dict(wavemaker=wm, inner_product=ip, path=path, vectors=(dRe, dIm, aRe, aIm))
+

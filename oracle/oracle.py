@@ -9,7 +9,7 @@ What it restates (each function cites the reference line it follows):
   ordering rules ``quicksort2`` / ``select_eigenvalues`` / ``sort_eigendecomp``: plain C in
   ``nekstab_oracle.c`` (reference operation order, no FP contraction);
 * the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
-  ``ts_gmres``, ``biorthogonalize``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
+  ``ts_gmres``, ``biorthogonalize``, ``wave_maker``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
   dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
 
 Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
@@ -450,6 +450,33 @@ def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):
     i = (gamma * aIm[:n] + delta * aRe[:n]) / den
     aRe[:n], aIm[:n] = r, i
     return dRe, dIm, aRe, aIm
+
+
+def wavemaker_pointwise(L: OLayout, dRe, dIm, aRe, aIm):
+    """sensitivity.f90:69-71 on reference-order vectors (velocity components c < ldim):
+    wk1 = sqrt(vx_dRe**2 + vx_dIm**2 + vy_dRe**2 + ...), wk2 likewise for the adjoint mode,
+    wavemaker = wk1*wk2.  Left-to-right sums as written (x**2 is the rounded x*x).  The 2-D
+    reference adds its uninitialised vz_* arrays (never copied when .not. if3D, :45-60); they are
+    taken as absent here."""
+    nv = L.nv
+    seg = lambda x, c: x[c * nv:(c + 1) * nv]  # noqa: E731
+    wk1 = seg(dRe, 0) ** 2 + seg(dIm, 0) ** 2
+    wk2 = seg(aRe, 0) ** 2 + seg(aIm, 0) ** 2
+    for c in range(1, L.ldim):
+        wk1 = wk1 + seg(dRe, c) ** 2
+        wk1 = wk1 + seg(dIm, c) ** 2
+        wk2 = wk2 + seg(aRe, c) ** 2
+        wk2 = wk2 + seg(aIm, c) ** 2
+    return np.sqrt(wk1) * np.sqrt(wk2)
+
+
+def wave_maker(L: OLayout, w, dRe, dIm, aRe, aIm):
+    """sensitivity.f90:3-77 after the four load_fld calls: ``ifto = ifpo = .false.`` (:40), so ``L``
+    is the velocity-only layout (the dots, opcmult and nopcopy see vx, vy, [vz]);
+    biorthogonalize (:63-66), then the pointwise product (:69-71).  Returns (wavemaker, the four
+    bi-orthogonalised vectors)."""
+    vecs = biorthogonalize(L, w, dRe, dIm, aRe, aIm)
+    return wavemaker_pointwise(L, *vecs), vecs
 
 
 def boostconv_core(state, rb, w, nv_total):

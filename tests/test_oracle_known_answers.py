@@ -8,6 +8,7 @@ solutions are exact, and against the one recorded run of the real reference (SUR
 """
 
 import numpy as np
+import pytest
 
 import oracle as orc
 from helpers import olayout, oracle_diag_matvec, oracle_rot2_matvec
@@ -113,6 +114,35 @@ def test_config5_biorthogonalize_property():
     re = ip(aRe, dRe) + ip(aIm, dIm)
     im = ip(aRe, dIm) - ip(aIm, dRe)
     assert abs(re - 1.0) < 1e-12 and abs(im) < 1e-12
+
+
+@pytest.mark.parametrize("ldim", [2, 3])
+def test_wave_maker_closed_form(ldim):
+    """wave_maker (sensitivity.f90:3-77) in closed form: bi-orthogonalisation scales the direct mode
+    d by 1/||d||_W and the adjoint mode a by 1/conj(<a, d/||d||>_W), so the pointwise product is
+    wm = |d| |a| / |<a, d>_W| (|.| the pointwise complex velocity modulus, <a, d> = (aRe.dRe +
+    aIm.dIm) + i (aRe.dIm - aIm.dRe)).  Hence wm does not change when either mode is multiplied
+    by a complex constant."""
+    lay = NekLayout(ldim=ldim, lx1=6, lx2=4, nelgv=9, n_scalars=0, ifpo=False)
+    L = orc.OLayout(lay.n_v, 0, ldim, False, ldim)
+    w = syn.mass_weights(lay)
+    vs = [syn.to_reference_order(lay, syn.hash_vector(lay, s)) for s in (5, 6, 7, 8)]
+    wm, _ = orc.wave_maker(L, w, *vs)
+    nv = lay.n_v
+    ww = np.tile(w[:nv] if w.size >= nv else w, ldim)[: ldim * nv]
+    ip = lambda p, q: float(np.sum(p[: ldim * nv] * ww * q[: ldim * nv]))  # noqa: E731
+    dRe, dIm, aRe, aIm = vs
+    ad = complex(ip(aRe, dRe) + ip(aIm, dIm), ip(aRe, dIm) - ip(aIm, dRe))
+    mod = lambda re, im: np.sqrt(sum(re[c * nv:(c + 1) * nv] ** 2 + im[c * nv:(c + 1) * nv] ** 2  # noqa: E731
+                                     for c in range(ldim)))
+    closed = mod(dRe, dIm) * mod(aRe, aIm) / abs(ad)
+    np.testing.assert_allclose(wm, closed, rtol=1e-12)
+    # a complex multiple of either mode leaves the wave-maker unchanged
+    c1, c2 = 2.5 - 0.7j, -0.3 + 1.9j
+    d2 = (c1.real * dRe - c1.imag * dIm, c1.real * dIm + c1.imag * dRe)
+    a2 = (c2.real * aRe - c2.imag * aIm, c2.real * aIm + c2.imag * aRe)
+    wm2, _ = orc.wave_maker(L, w, *d2, *a2)
+    np.testing.assert_allclose(wm2, wm, rtol=1e-12)
 
 
 def test_glsc3_is_sequential_sum():
