@@ -197,6 +197,30 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
                      double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream);
 
+/* ---- svds: Golub–Kahan–Lanczos with delayed re-orthogonalisation (f1; LightKrylov svds as called by
+ * transient_growth_analysis / resolvent_analysis, linear_stab.f90:112,153).  Two bases U, V, each
+ * read twice per step (a two-vector multi-dot and a dual update) instead of three times (CGS2).
+ * Step j (1-based; V col j-1 and U col j-2 provisional; C = projections of A V on U, D of A^T U on V):
+ *   f = A V[j-1];  j = 1: U[0] = f;  else
+ *     nkv_block_dot2(U, j-1, x=U[j-2], y=f, NKV_X_IS_LAST) -> h (all-reduce 2(j-1))
+ *     nkv_gkl_coef(0, j-2, h, h+(j-1), C, ...)  ->  coef;  C column j-3... finalised
+ *     nkv_dcgs2_update(U, j-2, coef, U[j-2], f, U[j-1], NULL)
+ *   f = A^T U[j-1];
+ *     nkv_block_dot2(V, j, x=V[j-1], y=f, NKV_X_IS_LAST) -> h (all-reduce 2j)
+ *     nkv_gkl_coef(1, j-1, h, h+j, D, ...);  nkv_dcgs2_update(V, j-1, coef, V[j-1], f, V[j], NULL)
+ * After step k each basis closes its provisional column: nkv_block_dot(Q, m+1, Q[m]) -> h,
+ * nkv_gkl_coef(side, m, h, NULL, ...), nkv_block_update(Q, m, coef+2m+5, Q[m]), nkv_normalize_dev(Q[m],
+ * coef+2m+3) with m = k-1 (U) and k (V).  Then A V_k = U_k C (k x k upper triangular) and
+ * A^T U_k = V_{k+1} D, both bases W-orthonormal.  The coefficient algebra (one workgroup):
+ *   a = hq[0:m], r = sqrt(hq[m] - a.a); with hw: M column p+1 (p = m - side) = [hw[0:m] ;
+ *   (hw[m] - a.hw[0:m])/r] (raw), coef = [hw[0:m]/r | . | 1/r, M(m,p+1)/r, r^2, 1 | a]; M column p
+ *   finalised (p >= 0): M[0:m,p] = (M[0:m,p] - M[0:m,0:p] A_other[:,p] + rho a)/r_other[p],
+ *   M[m,p] = rho r / r_other[p], rho = r_self[m-1] (1 at m = 0); A_self[:,m] = a, r_self[m] = r.
+ * M, A_self, A_other: device, column-major (ldm, lda >= m+1); r^2 <= 0 raises the NaN flag. */
+int nkv_gkl_coef(int side, int m, const double* hq_dev, const double* hw_dev, double* M_dev, int64_t ldm,
+                 double* A_self, double* r_self, const double* A_other, const double* r_other, int64_t lda,
+                 double* coef_dev, void* ws, void* stream);
+
 /* ---- the whole factorisation natively (a8: arnoldi_factorization, krylov_decomposition.f90:2-99 —
  * the loop :68-96 calling matvec then update_hessenberg_matrix) as ONE call: the DCGS2 sequence
  * above for mstep = mstart..mend, then the closing re-orthogonalisation, orchestrated in C++ (the

@@ -899,6 +899,89 @@ __global__ __launch_bounds__(kThreads) void k_dcgs2_coef(int m, const double* __
     }
 }
 
+// Golub–Kahan–Lanczos bidiagonalisation with delayed re-orthogonalisation (svds, nekStab's
+// transient_growth_analysis / resolvent_analysis, linear_stab.f90:112,153): two interleaved DCGS2
+// sequences.  The U side's "operator output" is A applied to V's PROVISIONAL vector, the V side's
+// is A^T applied to U's provisional vector; each side's pass finishes its own provisional vector
+// (re-orthogonalisation folded into the next pass over that basis) and projects the other side's
+// output once.  Projection coefficients are corrected one step later, when the provisional vector
+// they were formed from is finished.  One workgroup; side 0 = U (matrix M = C, A V = U C), side 1 =
+// V (M = D, A^T U = V D).  At pass m of a side (its basis holds m final columns and the provisional
+// one, column m):
+//   a = hq[0:m], r = sqrt(hq[m] - a.a)  (the provisional column's re-orthogonalisation)
+//   with hw (the other side's raw output f): raw coefficients b = hw[0:m],
+//     b_m = (hw[m] - a.b)/r into M column p+1 (p = m - side), and the dual-update coefficients
+//     coef = [x = b/r | c | rinv, y = b_m/r, r^2, s = 1 | a]  (f_out = f/r - Q_m x - qbar y);
+//   M column p finalised (p >= 0) from the other side's (a_o, r_o) at index p and this side's
+//     previous r (rho; 1 at m = 0):  M[0:m, p] = (M[0:m, p] - M[0:m, 0:p] a_o + rho a)/r_o,
+//     M[m, p] = rho r / r_o.
+// A_self / r_self receive (a, r) at index m (column m of A_self, leading dimension lda).
+__global__ __launch_bounds__(kThreads) void k_gkl_coef(int side, int m, const double* __restrict__ hq,
+                                                       const double* __restrict__ hw, double* __restrict__ M,
+                                                       int64_t ldm, double* __restrict__ As, double* __restrict__ rs,
+                                                       const double* __restrict__ Ao, const double* __restrict__ ro,
+                                                       int64_t lda, double* __restrict__ coef,
+                                                       int* __restrict__ nan_flag) {
+    __shared__ double lds4[4];
+    __shared__ double sc[2];
+    extern __shared__ double dyn[];
+    double* part = dyn;                                   // block_matvec partials: max(kThreads, m)
+    double* sg = part + (m > kThreads ? m : kThreads);    // M[0:m, 0:p] a_o
+    double* ca = coef + 2 * m + 5;
+    double s = 0.0, pab = 0.0;
+    for (int i = threadIdx.x; i < m; i += kThreads) {
+        const double ai = hq[i];
+        As[(int64_t)m * lda + i] = ai;
+        ca[i] = ai;
+        s = fma(ai, ai, s);
+        if (hw) pab = fma(ai, hw[i], pab);
+    }
+    s = block_sum(s, lds4);
+    __syncthreads();
+    if (threadIdx.x == 0) sc[0] = s;
+    __syncthreads();
+    pab = block_sum(pab, lds4);
+    __syncthreads();
+    if (threadIdx.x == 0) sc[1] = pab;
+    __syncthreads();
+    const double r2 = hq[m] - sc[0];
+    const double r = sqrt(r2), rinv = 1.0 / r;
+    const int p = m - side;
+    if (hw) {
+        double* Mq = M + (int64_t)(p + 1) * ldm;
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            const double bi = hw[i];
+            Mq[i] = bi;
+            coef[m + i] = bi;
+            coef[i] = bi * rinv;
+        }
+        if (threadIdx.x == 0) {
+            const double bm = (hw[m] - sc[1]) * rinv;
+            Mq[m] = bm;
+            coef[2 * m] = bm;
+            coef[2 * m + 2] = bm * rinv;
+        }
+    }
+    if (p >= 0) {
+        const double* ao = Ao + (int64_t)p * lda;
+        auto all = [](int) { return 0; };
+        auto to_p = [p](int) { return p; };
+        block_matvec(m, [M, ldm](int i, int c) { return M[(int64_t)c * ldm + i]; }, all, to_p, ao, part, sg);
+        const double rho = m > 0 ? rs[m - 1] : 1.0;
+        const double roi = 1.0 / ro[p];
+        double* Mp = M + (int64_t)p * ldm;
+        for (int i = threadIdx.x; i < m; i += kThreads) Mp[i] = fma(rho, hq[i], Mp[i] - sg[i]) * roi;
+        if (threadIdx.x == 0) Mp[m] = rho * r * roi;
+    }
+    if (threadIdx.x == 0) {
+        rs[m] = r;
+        coef[2 * m + 1] = rinv;
+        coef[2 * m + 3] = r2;
+        coef[2 * m + 4] = 1.0;
+        if (!(r2 > 0.0)) atomicOr(nan_flag, 1);   // breakdown: the provisional vector in span(Q_m)
+    }
+}
+
 // DCGS2 update, one read of Q_m (m columns):  qbar = (u s - Q_m a) * rinv  -> column m (in place),
 // f = (A u) s rinv - Q_m x - qbar * yc  -> fout (the next column: normalised one step later),
 // ||f||_W^2 partial.  One row tile (kTile rows at r0): returns f in af.
@@ -2130,6 +2213,23 @@ int nkv_dcgs2_coef_lazy(int m, const double* hq_dev, const double* hw_dev, const
     hipLaunchKernelGGL(k_dcgs2_coef, dim3(1), dim3(kThreads), dcgs2_coef_lds(m), S(stream), m, hq_dev, hw_dev,
                        nrm_prev_dev, H_dev,
                        ldh, coef_dev, T_dev, ldt, nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_gkl_coef(int side, int m, const double* hq_dev, const double* hw_dev, double* M_dev, int64_t ldm,
+                 double* A_self, double* r_self, const double* A_other, const double* r_other, int64_t lda,
+                 double* coef_dev, void* ws, void* stream) {
+    if (side != 0 && side != 1) return fail(NKV_EINVAL, "side=%d must be 0 (U) or 1 (V)", side);
+    if (m < 0 || m > NKV_MAX_COLS) return fail(NKV_EINVAL, "m=%d outside 0..%d", m, NKV_MAX_COLS);
+    if (!hq_dev || !M_dev || !A_self || !r_self || !coef_dev) return fail(NKV_EINVAL, "hq/M/A_self/r_self/coef is NULL");
+    if (m - side >= 0 && (!A_other || !r_other)) return fail(NKV_EINVAL, "A_other/r_other is NULL");
+    if (ldm < m + 1 || lda < m + 1) return fail(NKV_EINVAL, "ldm=%lld / lda=%lld < m+1=%d", (long long)ldm,
+                                                (long long)lda, m + 1);
+    CHECK(check_ptr(ws, "ws"));
+    const size_t lds = (size_t)((m > kThreads ? m : kThreads) + (m > 0 ? m : 1)) * sizeof(double);
+    hipLaunchKernelGGL(k_gkl_coef, dim3(1), dim3(kThreads), lds, S(stream), side, m, hq_dev, hw_dev, M_dev, ldm,
+                       A_self, r_self, A_other, r_other, lda, coef_dev, nan_flag_of(ws));
     NKV_LAUNCHED();
     return NKV_OK;
 }

@@ -14,9 +14,10 @@ clones `main`):
 LightKrylov's own arithmetic is not in the container, so these are restatements of the published
 algorithms with nekStab's call semantics — parity unpinned for this surface:
 ``eigs`` runs nekStab's Krylov–Schur (``krylov_schur.py``) in the caller's basis ``X``; ``svds`` is a
-k-step Golub–Kahan–Lanczos bidiagonalisation with full CGS2 re-orthogonalisation of both bases (the
-same block kernels; two bases resident, as BASELINE config 5); ``gmres`` is restarted GMRES stopping
-on ||r|| <= rtol ||b|| + atol.
+k-step Golub–Kahan–Lanczos bidiagonalisation with full re-orthogonalisation of both bases (two bases
+resident, as BASELINE config 5) — by default with delayed re-orthogonalisation (``"dcgs2"``: each
+basis read twice per step, one all-reduce per half-step), or CGS2 (three reads); ``gmres`` is
+restarted GMRES stopping on ||r|| <= rtol ||b|| + atol.
 """
 from __future__ import annotations
 
@@ -26,6 +27,7 @@ import numpy as np
 import torch
 
 from . import lapack
+from ._lib import NKV_TIME, NKV_X_IS_LAST
 from .arnoldi import HessenbergDev, arnoldi_factorization, orthonormalize
 from .config import KrylovSchurConfig
 from ._lib import NkvNaNError
@@ -96,10 +98,86 @@ class SvdsResult:
     breakdown: bool = False  # the bidiagonalisation reached an invariant subspace and was redone in MGS2
 
 
+def _gkl_dcgs2(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, k: int, Cd: HessenbergDev,
+               Dd: HessenbergDev) -> None:
+    """Golub–Kahan–Lanczos with delayed re-orthogonalisation (include/nekkrylov.h, nkv_gkl_coef): two
+    interleaved DCGS2 sequences.  The U side's operator output is A applied to V's provisional
+    vector, the V side's is A^T applied to U's; each pass over a basis finishes that basis's
+    provisional column (the second projection) and projects the other side's output once (the
+    first), so every vector is still projected twice, and each basis is read twice per step (a
+    two-vector multi-dot and a dual update) instead of three times.  The projection coefficients
+    of a provisional vector are corrected once it is finished (A ṽ = r A v + A V a, and A V = U C).
+    On return U[0:k], V[0:k+1] are final and W-orthonormal, Cd/Dd hold C and D as the CGS2 path
+    writes them.  V[0] (the seed) is renormalised in the first pass."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    f64 = dict(dtype=torch.float64, device=ctx.device)
+    ld = k + 1
+    AU, AV = torch.zeros((ld, ld), **f64), torch.zeros((ld, ld), **f64)
+    rU, rV = torch.zeros(ld, **f64), torch.zeros(ld, **f64)
+    Cd.t.zero_()
+    Dd.t.zero_()
+    cp = ctx.coef.data_ptr()
+    f = ctx.vector()
+    sides = {0: (U, Cd, AU, rU, AV, rV), 1: (V, Dd, AV, rV, AU, rU)}
+
+    def dual_pass(side, m, out_col):
+        Q, M, As, rs, Ao, ro = sides[side]
+        j = m + 1
+        h = ctx.hd[: 2 * j]
+        hp = h.data_ptr()
+        if tm:
+            tm.begin("block_dot2")
+        ctx.call("nkv_block_dot2", w, Q.ptr, j, Q.col_ptr(m), f.ptr, hp, ws, tf | NKV_X_IS_LAST, st)
+        if tm:
+            tm.end("block_dot2", 8.0 * (m * lay.N_w + 2 * lay.N_w + lay.n_v))
+        ctx.comm.allreduce_(h)
+        ctx.call_nl("nkv_gkl_coef", side, m, hp, hp + 8 * j, M.t.data_ptr(), ld, As.data_ptr(), rs.data_ptr(),
+                    Ao.data_ptr(), ro.data_ptr(), ld, cp, ws, st)
+        if tm:
+            tm.begin("dcgs2_update")
+        ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, Q.col_ptr(m), f.ptr, Q.col_ptr(out_col), None, ws, NKV_TIME, st)
+        if tm:
+            tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N))
+
+    def close(side, m):
+        Q, M, As, rs, Ao, ro = sides[side]
+        h = ctx.hd[: m + 1]
+        if tm:
+            tm.begin("block_dot")
+        ctx.call("nkv_block_dot", w, Q.ptr, m + 1, Q.col_ptr(m), h.data_ptr(), ws, tf, st)
+        if tm:
+            tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
+        ctx.comm.allreduce_(h)
+        ctx.call_nl("nkv_gkl_coef", side, m, h.data_ptr(), None, M.t.data_ptr(), ld, As.data_ptr(), rs.data_ptr(),
+                    Ao.data_ptr(), ro.data_ptr(), ld, cp, ws, st)
+        if m > 0:
+            if tm:
+                tm.begin("block_update")
+            ctx.call("nkv_block_update", w, Q.ptr, m, ctx.coef[2 * m + 5:].data_ptr(), Q.col_ptr(m), None, ws,
+                     NKV_TIME, st)
+            if tm:
+                tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
+        ctx.call("nkv_normalize_dev", Q.col_ptr(m), ctx.coef[2 * m + 3:].data_ptr(), None, 0, st)
+
+    A.matvec(V[0], U[0])            # step 1, U side: the first provisional u is A v_0 itself
+    for j in range(1, k + 1):
+        if j > 1:
+            A.matvec(V[j - 1], f)
+            dual_pass(0, j - 2, j - 1)
+        A.rmatvec(U[j - 1], f)
+        dual_pass(1, j - 1, j)
+    close(0, k - 1)
+    close(1, k)
+
+
 def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, tolerance: float,
-         mode: str = "cgs2", breakdown_tol: float = 1e-8) -> SvdsResult:
+         mode: str = "dcgs2", breakdown_tol: float = 1e-8) -> SvdsResult:
     """k-step Golub–Kahan–Lanczos bidiagonalisation with full re-orthogonalisation, k = len(U)-1.
     V[0] holds the prepared (normalised) seed.  A: ``matvec`` (direct) and ``rmatvec`` (adjoint).
+    ``mode``: ``"dcgs2"`` (default; delayed re-orthogonalisation, two reads of each basis per step,
+    see ``_gkl_dcgs2``), ``"cgs2"`` / ``"cgs2-native"`` (three reads), ``"mgs2"`` (reference order).
 
     A rank-deficient A makes the bidiagonalisation invariant before k steps (alpha_j or beta_j is
     rounding noise).  As in ``krylov_schur`` the classical modes cannot carry on from noise, so
@@ -113,12 +191,17 @@ def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, toler
     Dd = HessenbergDev(ctx, k)   # columns: projections of A^T u_j on v_1..v_{j+1}
     f = ctx.vector()
     broken = False
+    if mode in ("dcgs2", "dcgs2-native") and (k + 1 > ctx.max_cols or ctx.hd.numel() < 2 * (k + 1)):
+        raise ValueError(f"svds k={k} needs max_cols >= {k + 1}")
     while True:
-        for j in range(1, k + 1):
-            A.matvec(V[j - 1], f)
-            orthonormalize(ctx, U, j - 1, f, U.col_ptr(j - 1), Cd.col_ptr(j - 1), mode)
-            A.rmatvec(U[j - 1], f)
-            orthonormalize(ctx, V, j, f, V.col_ptr(j), Dd.col_ptr(j - 1), mode)
+        if mode in ("dcgs2", "dcgs2-native"):
+            _gkl_dcgs2(ctx, A, U, V, k, Cd, Dd)
+        else:
+            for j in range(1, k + 1):
+                A.matvec(V[j - 1], f)
+                orthonormalize(ctx, U, j - 1, f, U.col_ptr(j - 1), Cd.col_ptr(j - 1), mode)
+                A.rmatvec(U[j - 1], f)
+                orthonormalize(ctx, V, j, f, V.col_ptr(j), Dd.col_ptr(j - 1), mode)
         if mode in _MGS2:
             ctx.check_nan()
             break

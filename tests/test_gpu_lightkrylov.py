@@ -43,7 +43,8 @@ def _dense(ctx, A, w):
     return M, W, idx
 
 
-def test_svds_matches_dense_weighted_svd(gpu):
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+def test_svds_matches_dense_weighted_svd(gpu, mode):
     ctx, w, d, vh, A = _setup()
     M, W, idx = _dense(ctx, A, w)
     s_exact = np.linalg.svd(np.sqrt(W)[:, None] * M / np.sqrt(W)[None, :], compute_uv=False)
@@ -52,7 +53,7 @@ def test_svds_matches_dense_weighted_svd(gpu):
     seed = ctx.vector()
     seed.fill_hash(7)
     prepare_seed(seed, V[0])
-    r = svds(ctx, A, U, V, nev=3, tolerance=1e-8)
+    r = svds(ctx, A, U, V, nev=3, tolerance=1e-8, mode=mode)
     conv = r.residuals < 1e-8
     assert conv.sum() >= 3 and not r.breakdown
     np.testing.assert_allclose(r.sigma[:3], s_exact[:3], rtol=1e-10)
@@ -65,7 +66,7 @@ def test_svds_matches_dense_weighted_svd(gpu):
     assert np.sqrt(ctx.dot(Av, Av, False)) < 1e-9 * r.sigma[0]
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "cgs2-native"])
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "cgs2-native"])
 def test_svds_rank_deficient_breakdown(gpu, mode):
     """A rank-3 operator (three nonzero diagonal entries, W-self-adjoint, so the singular values are
     |d_i|) with k=12: the bidiagonalisation is invariant after 4 steps.  svds detects it (the
@@ -93,6 +94,45 @@ def test_svds_rank_deficient_breakdown(gpu, mode):
     A.matvec(v, Av)
     Av.axpby(1.0, u, -r.sigma[0])
     assert np.sqrt(ctx.dot(Av, Av, False)) < 1e-9 * r.sigma[0]
+
+
+@pytest.mark.parametrize("k", [1, 2, 17, 40])
+def test_svds_dcgs2_equals_cgs2(gpu, k):
+    """The delayed re-orthogonalisation (two reads of each basis per step) against the CGS2 path
+    (three reads) on the same operator and seed: the bidiagonal projections C, D agree to
+    1e-12 of their size, both bases are W-orthonormal to 1e-12, the relations A V_k = U_k C and
+    A^T U_k = V_{k+1} D hold to 1e-12, and sigma / singular vectors agree to 1e-10."""
+    ctx, w, d, vh, A = _setup()
+    out = {}
+    for mode in ("cgs2", "dcgs2"):
+        U, V = ctx.basis(k + 1), ctx.basis(k + 1)
+        seed = ctx.vector()
+        seed.fill_hash(7)
+        prepare_seed(seed, V[0])
+        r = svds(ctx, A, U, V, nev=1, tolerance=1e-8, mode=mode)
+        out[mode] = (r, U, V)
+    (rc, Uc, Vc), (rd, Ud, Vd) = out["cgs2"], out["dcgs2"]
+    np.testing.assert_allclose(rd.C, rc.C, rtol=0, atol=1e-12 * np.abs(rc.C).max())
+    np.testing.assert_allclose(rd.sigma, rc.sigma, rtol=1e-10, atol=1e-13 * rc.sigma[0])
+    for B, n in ((Ud, k), (Vd, k + 1)):
+        G = np.array([[ctx.dot(B[a], B[b], False) for b in range(n)] for a in range(n)])
+        assert np.abs(G - np.eye(n)).max() < 1e-12
+    x, y = ctx.vector(), ctx.vector()
+    for c in range(k):       # A v_c = sum_i C[i, c] u_i ;  A^T u_c = sum_i D[i, c] v_i
+        A.matvec(Vd[c], x)
+        get_vec(y, Ud, rd.C[:, c], k)
+        x.axpby(1.0, y, -1.0)
+        assert np.sqrt(ctx.dot(x, x, False)) < 1e-12 * max(1.0, np.abs(rd.C).max())
+    # leading singular vectors agree up to sign
+    u1, u2, v1, v2 = (ctx.vector() for _ in range(4))
+    get_vec(u1, Uc, rc.uvecs[:, 0], k)
+    get_vec(u2, Ud, rd.uvecs[:, 0], k)
+    get_vec(v1, Vc, rc.vvecs[:, 0], k)
+    get_vec(v2, Vd, rd.vvecs[:, 0], k)
+    sgn = np.sign(ctx.dot(u1, u2, False))
+    u1.axpby(1.0, u2, -sgn)
+    v1.axpby(1.0, v2, -sgn)
+    assert np.sqrt(ctx.dot(u1, u1, False)) < 1e-10 and np.sqrt(ctx.dot(v1, v1, False)) < 1e-10
 
 
 def test_eigs_and_get_vec(gpu):
