@@ -343,6 +343,15 @@ int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const 
 int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
                   double* out, int ncomp, void* stream);
 
+/* ---- ts_gmres host helper (a17, newton_krylov.f90:250-269) -------------------------------
+ * The least-squares residual ||beta e_1 - H(1:k+2, 1:k+1) y|| after one more Hessenberg column, in
+ * O(k) host work (Givens rotations; no device work, no stream).  h: H(0:k+1, k) (0-based column k,
+ * overwritten with its triangularised form), cs/sn: the k rotations so far (the new one appended at
+ * index k), g: k+2 doubles, g[0] = beta before the first column.  The reference solves the whole
+ * system with dgels at every column for this number (:255-258); y itself still comes from dgels on
+ * the final system. */
+double nkv_givens_column(int k, double* h, double* cs, double* sn, double* g);
+
 /* ---- shard-independent synthetic data ----------------------------------------------------
  * x[row] = 2*u - 1, u = hash(seed, field, global point) in [0,1) with 53 exact bits, for live
  * rows; padding rows = 0; time = 0.  Global point of local point i in a weighted field is

@@ -106,6 +106,7 @@ _SIGNATURES = {
     "nkv_op_cdiag": (c_int, [_L, _P, _P, _P, _P, c_int, _P]),
     "nkv_fill_hash": (c_int, [_L, _P, c_uint64, c_int64, c_int64, _P]),
     "nkv_wavemaker": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
+    "nkv_givens_column": (c_double, [c_int, _P, _P, _P, _P]),
     "nkv_gkl_coef": (c_int, [c_int, c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P]),
 }
 

@@ -2900,4 +2900,27 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
     return NKV_OK;
 }
 
+// Host function (no device work): one column of the GMRES least-squares residual update
+// (newton_krylov.f90:255-258 without solving for y).  h = H(0:k+1, k) of column k (0-based), cs/sn the
+// k rotations stored so far (rotation k is appended), g the rotated right-hand side (g[k], g[k+1]
+// updated; g[0] = beta on the first call).  Returns |g[k+1]| = ||beta e_1 - H y|| of the (k+2) x (k+1)
+// least-squares problem; h is overwritten with the triangularised column.
+double nkv_givens_column(int k, double* h, double* cs, double* sn, double* g) {
+    for (int i = 0; i < k; ++i) {
+        const double t = cs[i] * h[i] + sn[i] * h[i + 1];
+        h[i + 1] = -sn[i] * h[i] + cs[i] * h[i + 1];
+        h[i] = t;
+    }
+    const double a = h[k], b = h[k + 1];
+    const double r = std::hypot(a, b);
+    const double c = r == 0.0 ? 1.0 : a / r, s = r == 0.0 ? 0.0 : b / r;
+    cs[k] = c;
+    sn[k] = s;
+    h[k] = r;
+    h[k + 1] = 0.0;
+    g[k + 1] = -s * g[k];
+    g[k] = c * g[k];
+    return std::fabs(g[k + 1]);
+}
+
 }  // extern "C"

@@ -19,6 +19,13 @@ Differences, all documented in DESIGN.md: the orthogonalisation is the block CGS
 the Arnoldi step before it is read); when the inner loop runs to k_dim without converging the
 reference leaves ``k = k_dim+1`` and reads ``yvec(k_dim+1)`` out of bounds in ``k_matmul`` — here the
 update uses the k_dim columns that exist.
+
+Host work per inner iteration is O(k): the reference solves the whole (k+1) x k least-squares
+problem with dgels at every column only to test ||e - H y|| (:255-258).  That residual is the
+last entry of Q_k^T e after the Givens rotations that triangularise H (Saad alg. 6.9's own
+update), so each column applies the k-1 stored rotations to the new H column, forms one more,
+and reads the residual off; ``lstsq`` (dgels, the reference's call) runs once, on the final
+system, so y is the reference's.
 """
 from __future__ import annotations
 
@@ -26,11 +33,36 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import lapack
+from . import _lib, lapack
 from .arnoldi import HessenbergDev, arnoldi_factorization
 from .config import GmresConfig
 from .operators import LinearOperator
 from .vector import NekContext, NekVector, k_add2, k_copy, k_cmult, k_matmul, k_normalize, k_sub2
+
+
+class GivensResidual:
+    """||beta e_1 - H_k y_k|| of the GMRES least-squares problem, updated per Hessenberg column in
+    O(k): the rotations G_i that reduce H to upper-triangular R are stored, column k gets
+    G_{k-1} ... G_1 and a new rotation G_k zeroing H(k+1, k); g = G_k ... G_1 beta e_1, and the
+    least-squares residual is |g_{k+1}| (Saad, Iterative Methods, 2nd ed., prop. 6.9)."""
+
+    def __init__(self, beta: float, kmax: int):
+        self.cs = np.zeros(kmax)
+        self.sn = np.zeros(kmax)
+        self.g = np.zeros(kmax + 1)
+        self.g[0] = beta
+        self.h = np.zeros(kmax + 1)
+        self.k = 0
+        self._f = _lib.load().nkv_givens_column   # host C (include/nekkrylov.h): O(k), no device work
+        self._p = [a.ctypes.data for a in (self.h, self.cs, self.sn, self.g)]
+
+    def add_column(self, h: np.ndarray) -> float:
+        """h = H(1:k+1, k) of the next column k (0-based self.k); returns the residual norm."""
+        k = self.k
+        self.h[: k + 2] = h[: k + 2]
+        res = self._f(k, *self._p)
+        self.k = k + 1
+        return float(res)
 
 
 @dataclass
@@ -74,16 +106,17 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
         evec[0] = beta
         yvec = np.zeros(ks)
         k_used = ks
+        giv = GivensResidual(beta, ks)
         for k in range(1, ks + 1):
             arnoldi_factorization(ctx, op, Q, Hd, k, k, f=f, mode=cfg.mode)
             info.matvecs += 1
             H[: k + 1, k - 1] = Hd.t[k - 1, : k + 1].cpu().numpy()
-            yvec[:k] = lapack.lstsq(H[: k + 1, :k], evec[: k + 1])
-            beta = float(np.linalg.norm(evec[: k + 1] - H[: k + 1, :k] @ yvec[:k]))
+            beta = giv.add_column(H[: k + 1, k - 1])        # ||e - H y|| without solving for y
             info.inner_residuals.append(beta ** 2)
             k_used = k
             if beta ** 2 < cfg.tol or (cfg.findiff and beta ** 2 < 1e-8):
                 break
+        yvec[:k_used] = lapack.lstsq(H[: k_used + 1, :k_used], evec[: k_used + 1])   # :255, the final system
         ctx.check_nan()
         info.y_history.append(yvec[:k_used].copy())
         k_matmul(dq, Q, yvec[:k_used], k_used)

@@ -30,6 +30,7 @@ from . import lapack
 from ._lib import NKV_TIME, NKV_X_IS_LAST
 from .arnoldi import HessenbergDev, arnoldi_factorization, orthonormalize
 from .config import KrylovSchurConfig
+from .gmres import GivensResidual
 from ._lib import NkvNaNError
 from .krylov_schur import _MGS2, _mgs2_of, breakdown_column, krylov_schur
 from .operators import LinearOperator
@@ -256,15 +257,15 @@ def gmres(ctx: NekContext, A: LinearOperator, b: NekVector, x: NekVector, atol: 
         e[0] = beta
         H = np.zeros((kdim + 1, kdim))
         k_used = kdim
-        y = None
+        giv = GivensResidual(beta, kdim)
         for k in range(1, kdim + 1):
             arnoldi_factorization(ctx, A, Q, Hd, k, k, f=f, mode=mode, transpose=transpose)
             H[: k + 1, k - 1] = Hd.t[k - 1, : k + 1].cpu().numpy()
-            y = lapack.lstsq(H[: k + 1, :k], e[: k + 1])
-            res = float(np.linalg.norm(e[: k + 1] - H[: k + 1, :k] @ y))
+            res = giv.add_column(H[: k + 1, k - 1])     # O(k) per column; y solved once below
             k_used = k
             if res <= tol:
                 break
+        y = lapack.lstsq(H[: k_used + 1, :k_used], e[: k_used + 1])
         dq = ctx.vector()
         k_matmul(dq, Q, y, k_used)
         k_add2(x, dq)

@@ -155,3 +155,29 @@ def test_breakdown_column_rule():
     H[2, 1] = 1.0
     H[:, 5] = 0.0
     assert breakdown_column(H, 4, k, 1e-8) == 5
+
+
+def test_givens_residual_equals_least_squares_residual():
+    """gmres.GivensResidual: the O(k)-per-column residual of the GMRES least-squares problem equals
+    ||beta e_1 - H y|| with y from dgels (lapack.lstsq, the reference's newton_krylov.f90:255-258)
+    at every column, including an exactly zero subdiagonal (lucky breakdown: residual 0)."""
+    from nekstab_next_amd import lapack
+    from nekstab_next_amd.gmres import GivensResidual
+
+    rng = np.random.default_rng(3)
+    for trial in range(20):
+        k = int(rng.integers(1, 60))
+        H = np.triu(rng.standard_normal((k + 1, k)), -1)
+        H[np.arange(1, k + 1), np.arange(k)] = np.abs(H[np.arange(1, k + 1), np.arange(k)]) * 10.0 ** rng.uniform(-6, 0, k)
+        beta = float(rng.uniform(0.1, 10))
+        e = np.zeros(k + 1)
+        e[0] = beta
+        g = GivensResidual(beta, k)
+        for c in range(1, k + 1):
+            got = g.add_column(H[: c + 1, c - 1])
+            y = lapack.lstsq(np.asfortranarray(H[: c + 1, :c]), e[: c + 1])
+            ref = float(np.linalg.norm(e[: c + 1] - H[: c + 1, :c] @ y))
+            assert abs(got - ref) <= 1e-12 * beta + 1e-10 * ref, (trial, c, got, ref)
+    H = np.array([[2.0, 1.0], [0.0, 3.0], [0.0, 0.0]])   # H(2,1) = 0: exact after one column
+    g = GivensResidual(1.0, 2)
+    assert g.add_column(H[:2, 0]) == 0.0
