@@ -3,6 +3,12 @@
 grid size) and time the Gram–Schmidt entry points at BASELINE size in ONE process, interleaved
 over rounds (cdna_hip_programming.md §5.4 rule 24).
 
+Every variant is derived from the product source at build time: ``-D`` values of its speed knobs,
+and optionally a code experiment as a unified diff against it (``"patch": NAME`` applies
+``tools/experiments/NAME.patch`` to a copy of ``nekstab_next_amd/csrc/nekkrylov.hip``).  No copy of
+the kernel is kept: a patch that no longer applies fails the build (and the CPU test
+tests/test_product_source.py), and the unpatched variant is the product's own source.
+
   python tools/tune_kernels.py build            # here (hipcc cross-compiles)
   python tools/tune_kernels.py run [--E 44176]  # on the MI355X box
 """
@@ -16,6 +22,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "tools", "variants")
+PRODUCT_SRC = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
+EXP_DIR = os.path.join(ROOT, "tools", "experiments")
+HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include")]
 
 # Speed-only knobs of the product kernel.  The round-1 experiment switches (store skipping, soft
 # grid barriers, tile-interleaved / field-major sweeps, XCD maps, buffer-store policies, register-
@@ -112,21 +121,11 @@ VARIANTS = {
     "dc_r0": {"NKV_DC_ROUNDS": 0},
     "dc_r1": {"NKV_DC_ROUNDS": 1},
     "dc_r4": {"NKV_DC_ROUNDS": 4},
-    # round-2 experiment copy (tools/experiments/nekkrylov_exp.hip; earlier x_* variants: the dual-update
-    # and multi-dot row bands, logged in profiles/r02e-g_tune_*)
-    "x_base": {"src": "exp"},
-    "x_rf16_p2u4": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 2, "NKVX_ROTF_U16": 4},
-    "x_rf16_p2u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 2, "NKVX_ROTF_U16": 2},
-    "x_rf16_p1u8": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 1, "NKVX_ROTF_U16": 8},
-    "x_rf16_p4u2": {"src": "exp", "NKVX_ROTF16": 1, "NKVX_ROTF_P16": 4, "NKVX_ROTF_U16": 2},
-    "x_bd_r1": {"src": "exp", "NKVX_BD_ROUNDS": 1},
-    "x_bd_r2": {"src": "exp", "NKVX_BD_ROUNDS": 2},
-    "x_bd_r4": {"src": "exp", "NKVX_BD_ROUNDS": 4},
-    "x_bu_g768_r1": {"src": "exp", "NKVX_BU_G": 768, "NKVX_BU_ROUNDS": 1},
-    "x_bu_g768_r2": {"src": "exp", "NKVX_BU_G": 768, "NKVX_BU_ROUNDS": 2},
-    "x_bu_g1024_r1": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 1},
-    "x_bu_g1024_r2": {"src": "exp", "NKVX_BU_G": 1024, "NKVX_BU_ROUNDS": 2},
-    "x_rs_b128": {"src": "exp", "NKVX_ROTS_B128": 1},
+    # code experiments: unified diffs against the product source (tools/experiments/*.patch).  The
+    # round-2 experiment copy (NKVX_* switches: multi-dot / block-update row bands, conflict-free LDS
+    # rotation operands, few-column rotation at 9..16 columns) was retired in round 3; its logs stay
+    # under profiles/r02*_tune_*.
+    "fuse_fw_lds": {"patch": "fuse_fw_lds"},   # fused CGS2 pass: one wave loads f and w per tile
     "fmid512": {"NKV_FUSE_G_MID": 512},
     "fmid384": {"NKV_FUSE_G_MID": 384},
     "fmid768": {"NKV_FUSE_G_MID": 768},
@@ -138,17 +137,33 @@ VARIANTS = {
 }
 
 
+def variant_source(name: str, out_dir: str = VDIR) -> str:
+    """The variant's source file: the product source, with the variant's patch applied if it has
+    one (``patch`` fails loudly when the diff no longer applies)."""
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"src_{name}.hip")
+    pname = VARIANTS[name].get("patch")
+    if pname:
+        pf = os.path.join(EXP_DIR, pname + ".patch")
+        subprocess.run(["patch", "-s", "-o", out, PRODUCT_SRC, pf], check=True)
+    else:
+        with open(PRODUCT_SRC, "rb") as a, open(out, "wb") as b:
+            b.write(a.read())
+    return out
+
+
+def variant_defines(name: str) -> list:
+    return [f"-D{k}={v}" for k, v in VARIANTS[name].items() if k != "patch"]
+
+
 def build(names):
     os.makedirs(VDIR, exist_ok=True)
-    src = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
     procs = []
     for n in names:
-        defs = [f"-D{k}={v}" for k, v in VARIANTS[n].items() if k != "src"]
-        vsrc = (os.path.join(ROOT, "tools", "experiments", "nekkrylov_exp.hip") if VARIANTS[n].get("src") == "exp"
-                else src)
+        vsrc = variant_source(n)
         out = os.path.join(VDIR, f"lib_{n}.so")
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I" + os.path.join(ROOT, "include"), *defs, vsrc, "-o", out]
+        # the variant source sits in tools/variants/: the product's include directory is passed explicitly
+        cmd = ["/opt/rocm/bin/hipcc", *HIP_FLAGS, *variant_defines(n), vsrc, "-o", out]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
         assert p.wait() == 0
