@@ -164,11 +164,17 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         ctx.timer.end("finish", 16.0 * ctx.layout.N)
 
 
-def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool) -> None:
+def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool,
+                nrm2: torch.Tensor | None = None) -> None:
     """Step j (1-based) of DCGS2 Arnoldi: Q[0:j-1] final, Q[j-1] = u = beta q_j provisional and not
     yet normalised (unless ``first``: then u is normalised), f = A u.  On return Q[j-1] is final,
     Q[j] = the next u, H columns 0..j-2 final and column j-1 provisional, H(j, j-1) pending.
-    beta^2 = u^T W u is the last entry of the step's own Q^T W u, so one all-reduce per step."""
+    beta^2 = u^T W u is the last entry of the step's own Q^T W u, so one all-reduce per step.
+
+    ``nrm2`` (a 1-double device tensor): the update also forms ||next u||_W^2, fused, and all-reduces
+    it into ``nrm2`` (one more all-reduce); that value is then this step's H(j, j-1) estimate (per-
+    column consumers: the GMRES residual test) and the next step's beta^2.  Pass the same tensor
+    to every step of the factorisation."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     lay, tm = ctx.layout, ctx.timer
     tf = NKV_TIME if ctx.time_in_dot else 0
@@ -182,13 +188,16 @@ def _dcgs2_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVect
     if tm:
         tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef", m, hp, hp + 8 * j, None if first else hp + 8 * m, Hd.t.data_ptr(), Hd.k + 1, cp,
-                ws, st)
+    nprev = None if first else (nrm2.data_ptr() if nrm2 is not None else hp + 8 * m)
+    ctx.call_nl("nkv_dcgs2_coef", m, hp, hp + 8 * j, nprev, Hd.t.data_ptr(), Hd.k + 1, cp, ws, st)
     if tm:
         tm.begin("dcgs2_update")
-    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, u, f.ptr, Q.col_ptr(j), None, ws, NKV_TIME, st)
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, m, cp, u, f.ptr, Q.col_ptr(j), None if nrm2 is None else nrm2.data_ptr(),
+             ws, NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
     if tm:
-        tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N))
+        tm.end("dcgs2_update", 8.0 * (m * lay.N + 4 * lay.N) + (0.0 if nrm2 is None else 8.0 * lay.n_v))
+    if nrm2 is not None:
+        ctx.comm.allreduce_(nrm2)
 
 
 def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:

@@ -20,6 +20,15 @@ the Arnoldi step before it is read); when the inner loop runs to k_dim without c
 reference leaves ``k = k_dim+1`` and reads ``yvec(k_dim+1)`` out of bounds in ``k_matmul`` — here the
 update uses the k_dim columns that exist.
 
+Orthogonalisation (``GmresConfig.mode``): ``"dcgs2"`` runs the inner Arnoldi as ONE continuous
+DCGS2 factorisation (two reads of the basis per column instead of CGS2's three) with the norm of
+each new provisional vector fused into the update (``_dcgs2_step(nrm2=...)``), so the residual test
+of column k needs nothing from column k+1 — no lag, no extra matvec.  Column k's coefficients are
+then the once-projected ones (its re-orthogonalisation correction, O(eps) relative, arrives with the
+next column); the test uses them, and after the exit one closing multi-dot finalises the last
+column's row of H, so ``lstsq`` (dgels) sees an Arnoldi factorisation exact to rounding, as with
+CGS2.  ``"cgs2"`` / ``"mgs2"``: one finished column per step (``arnoldi_factorization(k, k)``).
+
 Host work per inner iteration is O(k): the reference solves the whole (k+1) x k least-squares
 problem with dgels at every column only to test ||e - H y|| (:255-258).  That residual is the
 last entry of Q_k^T e after the Givens rotations that triangularise H (Saad alg. 6.9's own
@@ -32,6 +41,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 import numpy as np
+import torch
 
 from . import _lib, lapack
 from .arnoldi import HessenbergDev, arnoldi_factorization
@@ -107,6 +117,27 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
         yvec = np.zeros(ks)
         k_used = ks
         giv = GivensResidual(beta, ks)
+        if cfg.mode == "dcgs2":
+            def stop(b):
+                info.inner_residuals.append(b ** 2)
+                return b ** 2 < cfg.tol or (cfg.findiff and b ** 2 < 1e-8)
+            k_used = dcgs2_cycle(ctx, op.matvec, Q, Hd, f, ks, giv, stop)
+            info.matvecs += k_used
+            H[: k_used + 1, :k_used] = Hd.download()[: k_used + 1, :k_used]
+            yvec[:k_used] = lapack.lstsq(H[: k_used + 1, :k_used], evec[: k_used + 1])
+            ctx.check_nan()
+            info.y_history.append(yvec[:k_used].copy())
+            k_matmul(dq, Q, yvec[:k_used], k_used)
+            k_add2(sol, dq)
+            k_copy(Q[0], sol)
+            beta = initialize_gmres_vector(ctx, op, Q[0], rhs, f)
+            info.matvecs += 1
+            info.outer_residuals.append(beta ** 2)
+            info.restarts = it + 1
+            if beta ** 2 < cfg.tol or (cfg.findiff and beta ** 2 < 1e-6):
+                info.converged = True
+                break
+            continue
         for k in range(1, ks + 1):
             arnoldi_factorization(ctx, op, Q, Hd, k, k, f=f, mode=cfg.mode)
             info.matvecs += 1
@@ -130,3 +161,35 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
             info.converged = True
             break
     return info
+
+
+def dcgs2_cycle(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: int, giv: GivensResidual,
+                stop) -> int:
+    """The inner loop (newton_krylov.f90:250-276) on one continuous DCGS2 factorisation
+    (``apply(x, y)``: y = A x; ``stop(residual)`` after every column).  Column k:
+    matvec on the provisional Q[k-1] (Q[0] normalised), one DCGS2 step with the fused norm, then the
+    residual estimate from H(0:k+1, k-1) — the step's once-projected coefficients and H(k, k-1) =
+    ||next u||_W.  On exit the closing multi-dot of Q[k] against Q[0:k+1] corrects H's row k and
+    fills in H(k, k-1) (nkv_dcgs2_coef without a second right-hand side); Q[k] itself is not needed
+    by the solution update and is left unfinished.  Returns the number of columns k."""
+    from .arnoldi import _dcgs2_step
+
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    nrm2 = ctx.scal[5:6]
+    k_used = ks
+    for k in range(1, ks + 1):
+        apply(Q[k - 1], f)
+        _dcgs2_step(ctx, Q, Hd, k, f, first=(k == 1), nrm2=nrm2)
+        Hd.t[k - 1, k].copy_(torch.sqrt(nrm2[0]))            # provisional H(k, k-1), on the device
+        beta = giv.add_column(Hd.t[k - 1, : k + 1].cpu().numpy())
+        k_used = k
+        if stop(beta):
+            break
+    m = k_used   # close: H row m corrected, H(m, m-1) from the fused norm (re-orthogonalised)
+    h = ctx.hd[: m + 1]
+    tf = _lib.NKV_TIME if ctx.time_in_dot else 0
+    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, Q.col_ptr(m), h.data_ptr(), ws, tf, st)
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, nrm2.data_ptr(), Hd.t.data_ptr(), Hd.k + 1,
+                ctx.coef.data_ptr(), ws, st)
+    return k_used

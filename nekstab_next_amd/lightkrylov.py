@@ -30,7 +30,7 @@ from . import lapack
 from ._lib import NKV_TIME, NKV_X_IS_LAST
 from .arnoldi import HessenbergDev, arnoldi_factorization, orthonormalize
 from .config import KrylovSchurConfig
-from .gmres import GivensResidual
+from .gmres import GivensResidual, dcgs2_cycle
 from ._lib import NkvNaNError
 from .krylov_schur import _MGS2, _mgs2_of, breakdown_column, krylov_schur
 from .operators import LinearOperator
@@ -232,7 +232,7 @@ def svds(ctx: NekContext, A: LinearOperator, U: Basis, V: Basis, nev: int, toler
 
 def gmres(ctx: NekContext, A: LinearOperator, b: NekVector, x: NekVector, atol: float = 1e-12,
           rtol: float = 1e-12, kdim: int = 30, maxiter: int = 10, transpose: bool = False,
-          mode: str = "cgs2"):
+          mode: str = "dcgs2"):
     """Restarted GMRES from the initial guess ``x`` (updated in place); stops when
     ||b - A x||_W <= rtol ||b||_W + atol.  Returns (info, residual_history); info = 0 converged."""
     Q = ctx.basis(kdim + 1)
@@ -258,6 +258,14 @@ def gmres(ctx: NekContext, A: LinearOperator, b: NekVector, x: NekVector, atol: 
         H = np.zeros((kdim + 1, kdim))
         k_used = kdim
         giv = GivensResidual(beta, kdim)
+        if mode == "dcgs2":   # one continuous DCGS2 factorisation, the residual test per column (gmres.py)
+            k_used = dcgs2_cycle(ctx, apply, Q, Hd, f, kdim, giv, lambda res: res <= tol)
+            H[: k_used + 1, :k_used] = Hd.download()[: k_used + 1, :k_used]
+            y = lapack.lstsq(H[: k_used + 1, :k_used], e[: k_used + 1])
+            dq = ctx.vector()
+            k_matmul(dq, Q, y, k_used)
+            k_add2(x, dq)
+            continue
         for k in range(1, kdim + 1):
             arnoldi_factorization(ctx, A, Q, Hd, k, k, f=f, mode=mode, transpose=transpose)
             H[: k + 1, k - 1] = Hd.t[k - 1, : k + 1].cpu().numpy()

@@ -196,7 +196,8 @@ def test_config3_full_size_hessenberg_vs_oracle(gpu):
         del Q
 
 
-@pytest.mark.parametrize("E,mode", [(1996, "cgs2"), (22728, "cgs2"), (1996, "cgs2-native")])
+@pytest.mark.parametrize("E,mode", [(1996, "cgs2"), (22728, "cgs2"), (1996, "cgs2-native"), (1996, "dcgs2"),
+                                    (22728, "dcgs2")])
 def test_config4_gmres_vs_oracle(gpu, E, mode):
     """Config 4: Newton–Krylov inner GMRES on J = D - I, k_dim=200, tol=1e-9 on beta**2
     (1cyl.usr:14, 1cyl.par:18,23), on the cylinder mesh (E=1996, N=175,648) and at BASELINE's
@@ -383,8 +384,9 @@ def test_krylov_schur_knobs(gpu):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
 
 
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
 @pytest.mark.parametrize("findiff", [False, True])
-def test_gmres_restarts_vs_oracle(gpu, findiff):
+def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
     """ts_gmres with a small Krylov space so the outer loop restarts (newton_krylov.f90:230-299):
     k_dim=8, maxiter=12 — inner and outer residual histories against the oracle (1e-8 relative),
     the same exits (findiff's relaxed 1e-8 inner / 1e-6 outer thresholds included), the solution
@@ -398,7 +400,7 @@ def test_gmres_restarts_vs_oracle(gpu, findiff):
     rhs = ctx.vector()
     rhs.fill_hash(3)
     sol = ctx.vector()
-    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=8, maxiter=12, tol=1e-12, findiff=findiff))
+    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=8, maxiter=12, tol=1e-12, findiff=findiff, mode=mode))
     J = syn.to_reference_order(lay, d) - 1.0
 
     def mv(x, y):

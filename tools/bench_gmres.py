@@ -56,19 +56,22 @@ def main():
     rhs = ctx.vector()
     rhs.fill_hash(3)
     sol = ctx.vector()
-    cfg = GmresConfig(k_dim=ks, maxiter=1, tol=1e-300)
     from nekstab_next_amd.profiling import PhaseTimer
 
-    ts_gmres(ctx, Timed(), rhs, sol, cfg)          # warm-up
-    torch.cuda.synchronize()
-    ctx.timer = PhaseTimer(ctx.device)
-    t0 = time.perf_counter()
-    info = ts_gmres(ctx, Timed(), rhs, sol, cfg)
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) * 1e3
-    ph = ctx.timer.summary()
-    ctx.timer = None
-    gpu_ms = sum(v["total_ms"] for v in ph.values())
+    rows = []
+    for mode in ("dcgs2", "cgs2"):
+        cfg = GmresConfig(k_dim=ks, maxiter=1, tol=1e-300, mode=mode)
+        ts_gmres(ctx, Timed(), rhs, sol, cfg)          # warm-up
+        torch.cuda.synchronize()
+        ctx.timer = PhaseTimer(ctx.device)
+        t0 = time.perf_counter()
+        info = ts_gmres(ctx, Timed(), rhs, sol, cfg)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        ph = ctx.timer.summary()
+        ctx.timer = None
+        gpu_ms = sum(v["total_ms"] for v in ph.values())
+        rows.append((mode, wall, gpu_ms, ph, info))
     # both residual forms on a Hessenberg matrix of the cycle's size (host only)
     H = np.asfortranarray(np.triu(np.random.default_rng(0).standard_normal((ks + 1, ks)), -1))
     e = np.zeros(ks + 1)
@@ -84,16 +87,17 @@ def main():
         g.add_column(H[: k + 1, k - 1])
     lapack.lstsq(H, e)
     givens_ms = (time.perf_counter() - t0) * 1e3
-    print(json.dumps(dict(
-        row="config4_gmres_cycle", N=lay.N, k_dim=ks, columns=len(info.inner_residuals), wall_ms=round(wall, 2),
-        gpu_ms=round(gpu_ms, 2), host_ms=round(wall - gpu_ms, 2), gpu_share=round(gpu_ms / wall, 3),
-        phases={k: dict(launches=v["launches"], total_ms=round(v["total_ms"], 2), gbps=round(v["gbps"], 1))
-                for k, v in ph.items()},
-        inner_residual_first_last=[info.inner_residuals[0], info.inner_residuals[-1]],
-        dgels_every_column_ms=round(dgels_ms, 2), givens_ms=round(givens_ms, 3),
-        note="gpu_ms = HIP events around the matvec and every Gram-Schmidt kernel family (busy time); "
-             "host_ms = wall - gpu_ms")),
-        flush=True)
+    for mode, wall, gpu_ms, ph, info in rows:
+        print(json.dumps(dict(
+            row="config4_gmres_cycle", mode=mode, N=lay.N, k_dim=ks, columns=len(info.inner_residuals),
+            wall_ms=round(wall, 2), gpu_ms=round(gpu_ms, 2), host_ms=round(wall - gpu_ms, 2),
+            gpu_share=round(gpu_ms / wall, 3),
+            phases={k: dict(launches=v["launches"], total_ms=round(v["total_ms"], 2), gbps=round(v["gbps"], 1))
+                    for k, v in ph.items()},
+            inner_residual_first_last=[info.inner_residuals[0], info.inner_residuals[-1]],
+            dgels_every_column_ms=round(dgels_ms, 2), givens_ms=round(givens_ms, 3),
+            note="gpu_ms = HIP events around the matvec and every Gram-Schmidt kernel family (busy time); "
+                 "host_ms = wall - gpu_ms")), flush=True)
 
 
 if __name__ == "__main__":
