@@ -344,3 +344,125 @@ def test_sharded_checkpoint_resumes_at_another_world_size(gpu, tmp_path, w_write
     assert Q_w.shape == Q_ref.shape
     assert np.max(np.abs(Q_w - Q_ref)) < 1e-12 * np.max(np.abs(Q_ref))
     assert np.max(np.abs(H_w - H_ref)) < 1e-12 * np.max(np.abs(H_ref))
+
+
+def _run_next(world_rank_pair, out, port, tmpdir):
+    """Round-3 paths on `world` gloo ranks: svds (delayed re-orthogonalisation of two bases), GMRES
+    on one continuous DCGS2 factorisation, and the wave-maker chain through multi-file mode sets."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import fld
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import GmresConfig, KrylovSchurConfig
+        from nekstab_next_amd.gmres import ts_gmres
+        from nekstab_next_amd.krylov_schur import krylov_schur, outpost_ks, prepare_seed
+        from nekstab_next_amd.layout import NekLayout, box3d_layout, cylinder_layout
+        from nekstab_next_amd.lightkrylov import svds
+        from nekstab_next_amd.operators import DiagOperator, RankTwoPerturbed, ShiftedOperator
+        from nekstab_next_amd.sensitivity import velocity_layout, wave_maker
+        from nekstab_next_amd.vector import NekContext
+
+        comm = Comm()
+        res = {}
+
+        def pert(ctx, base, scale, sigma):
+            vs = []
+            for s5 in (21, 22, 23, 24):
+                v = ctx.vector()
+                v.fill_hash(s5)
+                v.scal(scale)
+                vs.append(v)
+            return RankTwoPerturbed(base, *vs, sigma=sigma)
+
+        lay = NekLayout(ldim=2, lx1=4, lx2=2, nelgv=41, ifpo=False).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=comm, max_cols=48)
+        d, _ = syn.diag_spectrum(lay)
+        A = pert(ctx, DiagOperator(ctx, d), 0.05, 3.0)
+        k = 30
+        U, V = ctx.basis(k + 1), ctx.basis(k + 1)
+        seed = ctx.vector()
+        seed.fill_hash(7)
+        prepare_seed(seed, V[0])
+        r = svds(ctx, A, U, V, nev=3, tolerance=1e-8, mode="dcgs2")
+        res["svds"] = (r.sigma, r.C)
+
+        lay2 = cylinder_layout(203).shard(rank, world)
+        ctx2 = NekContext(lay2, weights=syn.mass_weights(lay2), comm=comm, max_cols=48)
+        d2, _ = syn.diag_spectrum(lay2)
+        op = ShiftedOperator(DiagOperator(ctx2, d2), -1.0)
+        rhs, sol, probe = ctx2.vector(), ctx2.vector(), ctx2.vector()
+        rhs.fill_hash(3)
+        probe.fill_hash(4)
+        info = ts_gmres(ctx2, op, rhs, sol, GmresConfig(k_dim=12, maxiter=20, tol=1e-14, mode="dcgs2"))
+        res["gmres"] = (info.inner_residuals, info.outer_residuals, ctx2.dot(sol, probe, False))
+
+        lay3 = box3d_layout(23).shard(rank, world)
+        ctx3 = NekContext(lay3, weights=syn.mass_weights(lay3), comm=comm, max_cols=32)
+        d3, _ = syn.diag_spectrum(lay3)
+        A3 = pert(ctx3, DiagOperator(ctx3, d3), 1e-3, 50.0)
+        seed3 = ctx3.vector()
+        seed3.fill_hash(11)
+        cfg = KrylovSchurConfig(k_dim=24, schur_tgt=2)
+        rd = krylov_schur(ctx3, A3, seed3, cfg)
+        ra = krylov_schur(ctx3, A3, seed3, cfg, transpose=True)
+        d_ = os.path.join(tmpdir, f"w{world}")
+        outpost_ks(ctx3, rd, d_, evop="d", maxmodes=1, session="mr", orthonormality=False)
+        outpost_ks(ctx3, ra, d_, evop="a", maxmodes=1, session="mr", orthonormality=False)
+        vlay = velocity_layout(box3d_layout(23)).shard(rank, world)
+        vctx = NekContext(vlay, weights=syn.mass_weights(vlay), comm=comm, max_cols=4)
+        wm = wave_maker(vctx, d_, session="mr", d_num=1, a_num=1)
+        comm.barrier()
+        g = np.zeros((23, vlay.pts_v))
+        for f in fld.read_fld_set(d_, "wm_", "mr", 1):   # every rank's file: the global field
+            g[f.emap - 1] = f.fields["t"]
+        res["wm"] = (wm["inner_product"], g)
+        out[(world, rank)] = res
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
+    """svds on delayed re-orthogonalisation, GMRES on DCGS2 and the wave-maker (multi-file mode sets
+    written and read by every rank) on `world` gloo ranks sharing the GPU reproduce the one-rank run:
+    singular values and C to 1e-12, GMRES histories 1e-8 (the oracle tests' gate) and the solution's projection 1e-12, the
+    complex <a, d>_W and the assembled wave-maker field to 1e-12."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_next, args=((0, 1), out, _free_port(), str(tmp_path)))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    port = _free_port()
+    procs = [ctx.Process(target=_run_next, args=((r, world), out, port, str(tmp_path))) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    one = out[(1, 0)]
+    for rank in range(world):
+        got = out[(world, rank)]
+        s1, C1 = one["svds"]
+        s2, C2 = got["svds"]
+        np.testing.assert_allclose(s2[:6], s1[:6], rtol=1e-12)
+        np.testing.assert_allclose(C2, C1, rtol=0, atol=1e-12 * np.abs(C1).max())
+        i1, o1, p1 = one["gmres"]
+        i2, o2, p2 = got["gmres"]
+        assert len(i1) == len(i2) and len(o1) == len(o2)
+        np.testing.assert_allclose(i2, i1, rtol=1e-8)   # as the oracle gate: partial-sum grouping only
+        np.testing.assert_allclose(o2, o1, rtol=1e-8)
+        assert abs(p2 - p1) <= 1e-12 * abs(p1)
+        ip1, g1 = one["wm"]
+        ip2, g2 = got["wm"]
+        assert abs(ip2 - ip1) <= 1e-12 * abs(ip1)
+        assert np.max(np.abs(g2 - g1)) <= 1e-12 * np.max(np.abs(g1))
