@@ -434,7 +434,7 @@ def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
     """svds on delayed re-orthogonalisation, GMRES on DCGS2 and the wave-maker (multi-file mode sets
     written and read by every rank) on `world` gloo ranks sharing the GPU reproduce the one-rank run:
     singular values and C to 1e-12, GMRES histories 1e-8 (the oracle tests' gate) and the solution's projection 1e-12, the
-    complex <a, d>_W and the assembled wave-maker field to 1e-12."""
+    modulus of <a, d>_W and the assembled wave-maker field to 1e-12."""
     mgr = mp.Manager()
     out = mgr.dict()
     ctx = mp.get_context("spawn")
@@ -464,5 +464,7 @@ def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
         assert abs(p2 - p1) <= 1e-12 * abs(p1)
         ip1, g1 = one["wm"]
         ip2, g2 = got["wm"]
-        assert abs(ip2 - ip1) <= 1e-12 * abs(ip1)
+        # the eigenvectors' free phase (dgeev's sign) may differ between world sizes: |<a, d>| and the
+        # wave-maker field do not depend on it
+        assert abs(abs(ip2) - abs(ip1)) <= 1e-12 * abs(ip1)
         assert np.max(np.abs(g2 - g1)) <= 1e-12 * np.max(np.abs(g1))
