@@ -247,6 +247,26 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
                       int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec, void* mv_user,
                       nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
 
+/* ts_gmres's inner loop (a17: newton_krylov.f90:250-276, each column arnoldi_factorization(Q,H,k,k)
+ * then lstsq and norm2(e - H y)) as ONE call on a continuous DCGS2 factorisation: per column k the
+ * DCGS2 step of nkv_arnoldi_dcgs2 with the norm of the next provisional vector fused into the update
+ * (one more all-reduce), the least-squares residual from nkv_givens_column on H(0:k+1, k-1) with
+ * H(k, k-1) = that norm (the column's once-projected coefficients: its O(eps) re-orthogonalisation
+ * correction arrives with the next column, so the test needs no lag and no extra matvec), stored in
+ * res_hist[k-1]; stop when res^2 < tol2 (the reference's beta**2 < tol, or max(tol, 1e-8) for its
+ * iffindiff exit) or at kmax.  Then one closing multi-dot finalises H's last row.
+ *   On entry Q column 0 = r0 / beta (W-normalised), beta = ||r0||_W.  On return *k_out = k columns,
+ *   H_dev (column-major, ldh >= kmax+1) holds the (k+1) x k Hessenberg matrix of A Q_k = Q_{k+1} H;
+ *   Q columns 0..k-1 are final (column k is left unfinished: the solution update does not read it).
+ *   The host then solves y = lstsq(H, beta e_1) (dgels, lapack_wrapper.f90:248-300, as the reference)
+ *   and forms sol += Q_k y (nkv_combine).  res_hist: kmax host doubles.  scratch_dev:
+ *   nkv_arnoldi_scratch_doubles(kmax) doubles; ws: nkv_workspace_bytes(L, kmax + 1).  Callbacks and
+ *   flags (NKV_TIME_DOT) as nkv_arnoldi_dcgs2. */
+int nkv_gmres_dcgs2(const nkv_layout* L, const double* w, double* Q, int kmax, double beta, double tol2,
+                    double* H_dev, int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
+                    void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, double* res_hist, int* k_out,
+                    unsigned flags, void* stream);
+
 /* update_hessenberg_matrix(H, f, Q, k) itself as one call (krylov_decomposition.f90:103-189): the
  * fused 3-pass CGS2 sequence of the block Gram–Schmidt section above (block_dot, all-reduce,
  * block_update_dot, all-reduce, block_update + norm, all-reduce, arnoldi_finish) with the

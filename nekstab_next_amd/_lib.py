@@ -91,6 +91,8 @@ _SIGNATURES = {
     "nkv_arnoldi_dcgs2": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P, ALLREDUCE_FN, _P,
                                   c_uint, _P]),
     "nkv_update_hessenberg": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, _P, ALLREDUCE_FN, _P, c_uint, _P]),
+    "nkv_gmres_dcgs2": (c_int, [_L, _P, _P, c_int, c_double, c_double, _P, c_int64, _P, _P, _P, MATVEC_FN, _P,
+                                ALLREDUCE_FN, _P, _P, _P, c_uint, _P]),
     "nkv_arnoldi_factorization": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P,
                                           ALLREDUCE_FN, _P, c_uint, _P]),
     "nkv_combine": (c_int, [_L, _P, c_int, _P, _P, c_uint, _P]),

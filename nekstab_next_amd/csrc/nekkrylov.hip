@@ -2409,6 +2409,72 @@ int nkv_arnoldi_dcgs2(const nkv_layout* L, const double* w, double* Q, int mstar
     return (flags & NKV_CHECK_BREAKDOWN) ? check_breakdown(H_dev, ldh, mstart - 1, mend, ws, stream) : NKV_OK;
 }
 
+// ts_gmres's inner loop (newton_krylov.f90:250-276) as one call: one continuous DCGS2 factorisation with
+// the norm of every new provisional vector fused into the update, the least-squares residual of each
+// column from nkv_givens_column on the host, and the closing multi-dot that finalises H's last row
+// (the orchestration of nekstab_next_amd/gmres.py dcgs2_cycle, same entry points in the same order).
+int nkv_gmres_dcgs2(const nkv_layout* L, const double* w, double* Q, int kmax, double beta, double tol2,
+                    double* H_dev, int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
+                    void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, double* res_hist, int* k_out,
+                    unsigned flags, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(Q, "Q"));
+    CHECK(check_ptr(f, "f"));
+    CHECK(check_ptr(w, "w"));
+    CHECK(check_ptr(ws, "ws"));
+    if (!matvec) return fail(NKV_EINVAL, "matvec callback is NULL");
+    if (!H_dev || !scratch_dev || !res_hist || !k_out) return fail(NKV_EINVAL, "H/scratch/res_hist/k_out is NULL");
+    if (kmax < 1 || kmax + 1 > NKV_MAX_COLS) return fail(NKV_EINVAL, "kmax=%d outside 1..%d", kmax, NKV_MAX_COLS - 1);
+    if (ldh < kmax + 1) return fail(NKV_EINVAL, "ldh=%lld < kmax+1=%d", (long long)ldh, kmax + 1);
+    hipStream_t st = S(stream);
+    const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+    double* hd = scratch_dev;                                      // 2(kmax+1)
+    double* coef = scratch_dev + 2 * (kmax + 1);                   // 3 kmax + 5
+    double* nrm2 = scratch_dev + nkv_arnoldi_scratch_doubles(kmax) - 1;
+    double* host = static_cast<double*>(malloc(sizeof(double) * (size_t)(4 * (kmax + 2))));
+    if (!host) return fail(NKV_EINVAL, "gmres: host allocation failed");
+    double *h = host, *cs = host + (kmax + 2), *sn = cs + (kmax + 2), *g = sn + (kmax + 2);
+    for (int i = 0; i < kmax + 2; ++i) g[i] = 0.0;
+    g[0] = beta;
+    auto col = [L, Q](int c) { return Q + (int64_t)c * L->ld; };
+    auto reduce = [&](double* buf, int n, const char* what) -> int {
+        if (!allreduce) return NKV_OK;
+        const int rc = allreduce(ar_user, buf, n, stream);
+        return rc == 0 ? NKV_OK : fail(NKV_ECALLBACK, "allreduce callback returned %d (%s)", rc, what);
+    };
+    int rc = NKV_OK, k_used = kmax;
+    for (int k = 1; k <= kmax && rc == NKV_OK; ++k) {
+        const int m = k - 1;
+        double* u = col(m);
+        const int mr = matvec(mv_user, u, f, stream);
+        if (mr != 0) { rc = fail(NKV_ECALLBACK, "matvec callback returned %d at column %d", mr, k); break; }
+        if ((rc = nkv_block_dot2(L, w, Q, k, u, f, hd, ws, tf | NKV_X_IS_LAST, stream)) != NKV_OK) break;
+        if ((rc = reduce(hd, 2 * k, "multi-dot")) != NKV_OK) break;
+        if ((rc = nkv_dcgs2_coef(m, hd, hd + k, k == 1 ? nullptr : nrm2, H_dev, ldh, coef, ws, stream)) != NKV_OK) break;
+        if ((rc = nkv_dcgs2_update(L, w, Q, m, coef, u, f, col(k), nrm2, ws, NKV_TIME | (flags & NKV_TIME_DOT),
+                                   stream)) != NKV_OK) break;
+        if ((rc = reduce(nrm2, 1, "norm")) != NKV_OK) break;
+        // H(0:k, k-1) (once-projected) and ||next u||^2 -> the residual test of column k
+        hipError_t e = hipMemcpyAsync(h, H_dev + (int64_t)m * ldh, sizeof(double) * (size_t)k, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(h + k, nrm2, sizeof(double), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { rc = fail(NKV_EHIP, "gmres: %s", hipGetErrorString(e)); break; }
+        h[k] = sqrt(h[k]);
+        const double res = nkv_givens_column(m, h, cs, sn, g);
+        res_hist[m] = res;
+        k_used = k;
+        if (res * res < tol2) break;
+    }
+    free(host);
+    if (rc != NKV_OK) return rc;
+    *k_out = k_used;
+    // close: Q column k_used against Q[0:k_used+1] -> H row k_used corrected, H(k_used, k_used-1) final
+    const int m = k_used;
+    CHECK(nkv_block_dot(L, w, Q, m + 1, col(m), hd, ws, tf, stream));
+    CHECK(reduce(hd, m + 1, "closing multi-dot"));
+    return nkv_dcgs2_coef(m, hd, nullptr, nrm2, H_dev, ldh, coef, ws, stream);
+}
+
 // update_hessenberg_matrix (krylov_decomposition.f90:103-189) as one call: the fused 3-pass CGS2
 // sequence of nekstab_next_amd/arnoldi.py (orthonormalize, mode "cgs2") with the all-reduce as a
 // callback — q_out = f/||f|| after two projections, H column in hcol_dev[0:j+1].

@@ -117,11 +117,16 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
         yvec = np.zeros(ks)
         k_used = ks
         giv = GivensResidual(beta, ks)
-        if cfg.mode == "dcgs2":
-            def stop(b):
-                info.inner_residuals.append(b ** 2)
-                return b ** 2 < cfg.tol or (cfg.findiff and b ** 2 < 1e-8)
-            k_used = dcgs2_cycle(ctx, op.matvec, Q, Hd, f, ks, giv, stop)
+        if cfg.mode in ("dcgs2", "dcgs2-native"):
+            if cfg.mode == "dcgs2":
+                def stop(b):
+                    info.inner_residuals.append(b ** 2)
+                    return b ** 2 < cfg.tol or (cfg.findiff and b ** 2 < 1e-8)
+                k_used = dcgs2_cycle(ctx, op.matvec, Q, Hd, f, ks, giv, stop)
+            else:   # the same cycle as ONE library call (nkv_gmres_dcgs2), bit-identical
+                tol2 = max(cfg.tol, 1e-8) if cfg.findiff else cfg.tol
+                k_used, res = gmres_cycle_native(ctx, op.matvec, Q, Hd, f, ks, beta, tol2)
+                info.inner_residuals.extend(float(r) ** 2 for r in res)
             info.matvecs += k_used
             H[: k_used + 1, :k_used] = Hd.download()[: k_used + 1, :k_used]
             yvec[:k_used] = lapack.lstsq(H[: k_used + 1, :k_used], evec[: k_used + 1])
@@ -193,3 +198,41 @@ def dcgs2_cycle(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: 
     ctx.call_nl("nkv_dcgs2_coef", m, h.data_ptr(), None, nrm2.data_ptr(), Hd.t.data_ptr(), Hd.k + 1,
                 ctx.coef.data_ptr(), ws, st)
     return k_used
+
+
+def gmres_cycle_native(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: int, beta: float,
+                       tol2: float):
+    """``dcgs2_cycle`` as ONE library call (``nkv_gmres_dcgs2``, include/nekkrylov.h): the operator
+    and the all-reduce as callbacks, the per-column residuals returned.  Returns (k, residuals)."""
+    import ctypes
+
+    from .arnoldi import _allreduce_callback, _native_scratch
+
+    scratch = _native_scratch(ctx, ks)
+    base, ld8, fptr = Q.ptr, 8 * ctx.layout.ld, f.ptr
+    errors = []
+
+    def matvec(_user, x, y, _stream):
+        try:
+            c, r = divmod((x or 0) - base, ld8)
+            if r or not 0 <= c < Q.k or y != fptr:
+                raise ValueError(f"nkv_gmres_dcgs2 matvec callback: x={x}, y={y} are not a basis column and f")
+            apply(Q[c], f)
+            return 0
+        except BaseException as e:  # noqa: BLE001 — surfaced after the call returns
+            errors.append(e)
+            return 1
+
+    mv_c = _lib.MATVEC_FN(matvec)
+    ar_c = _allreduce_callback(ctx, scratch, errors)
+    res = np.zeros(ks)
+    k_out = ctypes.c_int(0)
+    rc = ctx.lib.nkv_gmres_dcgs2(ctx._Lp, ctx.w.data_ptr(), Q.ptr, int(ks), float(beta), float(tol2),
+                                 Hd.t.data_ptr(), Hd.k + 1, fptr, scratch.data_ptr(), ctx.ws.data_ptr(), mv_c, None,
+                                 ar_c, None, res.ctypes.data, ctypes.addressof(k_out),
+                                 _lib.NKV_TIME_DOT if ctx.time_in_dot else 0, ctx.stream)
+    if errors:
+        raise errors[0]
+    _lib.check(rc, "nkv_gmres_dcgs2")
+    k = int(k_out.value)
+    return k, res[:k]

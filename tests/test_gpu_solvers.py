@@ -197,7 +197,7 @@ def test_config3_full_size_hessenberg_vs_oracle(gpu):
 
 
 @pytest.mark.parametrize("E,mode", [(1996, "cgs2"), (22728, "cgs2"), (1996, "cgs2-native"), (1996, "dcgs2"),
-                                    (22728, "dcgs2")])
+                                    (22728, "dcgs2"), (1996, "dcgs2-native")])
 def test_config4_gmres_vs_oracle(gpu, E, mode):
     """Config 4: Newton–Krylov inner GMRES on J = D - I, k_dim=200, tol=1e-9 on beta**2
     (1cyl.usr:14, 1cyl.par:18,23), on the cylinder mesh (E=1996, N=175,648) and at BASELINE's
@@ -384,7 +384,7 @@ def test_krylov_schur_knobs(gpu):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-native"])
 @pytest.mark.parametrize("findiff", [False, True])
 def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
     """ts_gmres with a small Krylov space so the outer loop restarts (newton_krylov.f90:230-299):
@@ -532,3 +532,26 @@ def test_factorisation_is_run_to_run_deterministic(gpu, mode):
     np.testing.assert_array_equal(H1, H2)
     assert np.all(np.abs(np.diag(H1, -1)) > 0)
     assert torch.equal(Q1.storage, Q2.storage)
+
+
+def test_gmres_native_cycle_is_bit_identical(gpu):
+    """nkv_gmres_dcgs2 (the inner loop as one library call, for C/Fortran hosts) runs the same entry
+    points in the same order as the Python-driven dcgs2 cycle: residual histories, solution and
+    the final Hessenberg matrix are identical bit for bit."""
+    lay = cylinder_layout(300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=40)
+    d, _ = syn.diag_spectrum(lay)
+    op = ShiftedOperator(DiagOperator(ctx, d), -1.0)
+    rhs = ctx.vector()
+    rhs.fill_hash(3)
+    out = {}
+    for mode in ("dcgs2", "dcgs2-native"):
+        sol = ctx.vector()
+        info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=16, maxiter=6, tol=1e-20, mode=mode))
+        out[mode] = (info.inner_residuals, info.outer_residuals, sol.to_packed(), info.y_history)
+    a, b = out["dcgs2"], out["dcgs2-native"]
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_array_equal(a[2], b[2])
+    for ya, yb in zip(a[3], b[3]):
+        np.testing.assert_array_equal(ya, yb)
