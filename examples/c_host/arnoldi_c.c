@@ -14,7 +14,11 @@
  * Q and H bit for bit.  Last, the breakdown protocol of include/nekkrylov.h on a rank-3 operator:
  * nkv_arnoldi_dcgs2 with NKV_CHECK_BREAKDOWN returns NKV_EBREAKDOWN, the host restores the seed
  * column and redoes the factorisation with nkv_arnoldi_factorization(NKV_MGS2) (the reference's
- * order), whose basis must be W-orthonormal.  Exit status 0 on success.
+ * order), whose basis must be W-orthonormal.  Then ts_gmres's inner loop as one call
+ * (nkv_gmres_dcgs2) on the diagonal operator: the host solves the small least-squares problem (here
+ * by Givens + back substitution; a Fortran host calls its lstsq/dgels), forms x = Q y with
+ * nkv_combine and checks that ||b - A x||_W equals the last reported residual.  Exit status 0 on
+ * success.
  */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -204,8 +208,67 @@ int main(int argc, char** argv) {
     HK(hipMemcpy(H2, Hd2, (size_t)m * (m + 1) * sizeof(double), hipMemcpyDeviceToHost));
     printf("arnoldi_c: MGS2 fallback: H(5,4) = %.3e (span{q1, A q1, ...} invariant after 4 steps), max|Q^T W Q - I| = %.3e\n",
            H2[3 * (m + 1) + 4], orth2);
+    const double h54 = H2[3 * (m + 1) + 4];
+    /* ts_gmres inner loop as ONE call: A x = b with the well-conditioned diagonal of the first part
+       (d in (0.05, 1)); Q column 0 = b / ||b||_W */
+    HK(hipMemcpyAsync(d, hdg, vbytes, hipMemcpyHostToDevice, st));   /* hdg holds the rank-3 diagonal now: */
+    CK(nkv_fill_hash(&L, d, 99, 0, 0, st));                           /* rebuild d in (0.05, 1)            */
+    HK(hipMemcpyAsync(hdg, d, vbytes, hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < L.ld; ++i) hdg[i] = 0.525 + 0.475 * hdg[i];
+    HK(hipMemcpyAsync(d, hdg, vbytes, hipMemcpyHostToDevice, st));
+    double *b, *x;
+    HK(hipMalloc((void**)&b, vbytes));
+    HK(hipMalloc((void**)&x, vbytes));
+    HK(hipMemsetAsync(b, 0, vbytes, st));
+    CK(nkv_fill_hash(&L, b, 3, 0, 0, st));
+    CK(nkv_dot(&L, w, b, b, nrm, ws, 0, st));
+    double bb;
+    HK(hipMemcpyAsync(&bb, nrm, sizeof(double), hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    const double beta = sqrt(bb);
+    HK(hipMemsetAsync(Q2, 0, (size_t)(m + 1) * vbytes, st));
+    HK(hipMemsetAsync(Hd2, 0, (size_t)m * (m + 1) * sizeof(double), st));
+    HK(hipMemcpyAsync(Q2, b, vbytes, hipMemcpyDeviceToDevice, st));
+    CK(nkv_normalize_dev(&L, Q2, nrm, NULL, 0, st));
+    double* res = (double*)calloc((size_t)m, sizeof(double));
+    int kk = 0;
+    CK(nkv_gmres_dcgs2(&L, w, Q2, m, beta, 1e-24, Hd2, m + 1, f, scr, ws, diag_matvec, &op, NULL, NULL, res, &kk, 0, st));
+    HK(hipMemcpyAsync(H2, Hd2, (size_t)m * (m + 1) * sizeof(double), hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    /* least squares min ||beta e1 - H y||: Givens (nkv_givens_column) then R y = g */
+    double *cs = (double*)calloc((size_t)m + 2, sizeof(double)), *sn = (double*)calloc((size_t)m + 2, sizeof(double));
+    double *gv = (double*)calloc((size_t)m + 2, sizeof(double)), *R = (double*)calloc((size_t)(m + 2) * m, sizeof(double));
+    double* y = (double*)calloc((size_t)m, sizeof(double));
+    gv[0] = beta;
+    double lsres = 0.0;
+    for (int c = 0; c < kk; ++c) {
+        double* rc = R + (size_t)c * (m + 2);
+        for (int r = 0; r <= c + 1; ++r) rc[r] = H2[(size_t)c * (m + 1) + r];
+        lsres = nkv_givens_column(c, rc, cs, sn, gv);
+    }
+    for (int r = kk - 1; r >= 0; --r) {
+        double v = gv[r];
+        for (int c = r + 1; c < kk; ++c) v -= R[(size_t)c * (m + 2) + r] * y[c];
+        y[r] = v / R[(size_t)r * (m + 2) + r];
+    }
+    double* yd;
+    HK(hipMalloc((void**)&yd, (size_t)m * sizeof(double)));
+    HK(hipMemcpyAsync(yd, y, (size_t)kk * sizeof(double), hipMemcpyHostToDevice, st));
+    CK(nkv_combine(&L, Q2, kk, yd, x, 0, st));                      /* x = Q_k y */
+    CK(nkv_op_diag(&L, d, x, f, 0.0, st));                          /* f = A x - b */
+    CK(nkv_axpby(&L, f, 1.0, b, -1.0, 0, st));
+    CK(nkv_dot(&L, w, f, f, nrm, ws, 0, st));
+    double rr;
+    HK(hipMemcpyAsync(&rr, nrm, sizeof(double), hipMemcpyDeviceToHost, st));
+    HK(hipStreamSynchronize(st));
+    const double true_res = sqrt(rr);
+    printf("arnoldi_c: nkv_gmres_dcgs2: %d columns, reported residual %.3e, least-squares %.3e, ||b - A x||_W = %.3e "
+           "(||b|| = %.3e)\n", kk, res[kk - 1], lsres, true_res, beta);
+    const int gm_ok = kk == m && fabs(true_res - lsres) <= 1e-10 * beta && fabs(res[kk - 1] - lsres) <= 1e-12 * beta &&
+                      lsres < 1e-3 * beta;
     const int ok = orth < 1e-12 && arn / hmax < 1e-12 && same && rb == NKV_EBREAKDOWN && orth2 < 1e-8 &&
-                   fabs(H2[3 * (m + 1) + 4]) < 1e-12;
+                   fabs(h54) < 1e-12 && gm_ok;
     printf(ok ? "arnoldi_c: OK\n" : "arnoldi_c: FAILED\n");
     (void)rows;
     return ok ? 0 : 1;

@@ -104,6 +104,20 @@ module nkv_bindings
          integer(c_int64_t), value :: ldh
          type(c_funptr), value :: matvec, allreduce
       end function
+      ! ts_gmres's inner loop (newton_krylov.f90:250-276) as one call: k_out columns, res_hist(1:k_out) the
+      ! per-column least-squares residuals; the host then calls lstsq (dgels) on H and nkv_combine
+      integer(c_int) function nkv_gmres_dcgs2(L, w, Q, kmax, beta, tol2, H, ldh, f, scratch, ws, matvec, mv_user, &
+            allreduce, ar_user, res_hist, k_out, flags, stream) bind(C, name="nkv_gmres_dcgs2")
+         import :: c_int, c_int64_t, c_double, c_ptr, c_funptr, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: w, Q, H, f, scratch, ws, mv_user, ar_user, stream
+         integer(c_int), value :: kmax, flags
+         real(c_double), value :: beta, tol2
+         integer(c_int64_t), value :: ldh
+         type(c_funptr), value :: matvec, allreduce
+         real(c_double), intent(out) :: res_hist(*)
+         integer(c_int), intent(out) :: k_out
+      end function
       ! per-column factorisation (CGS2, or the reference's MGS2 order with NKV_MGS2): same arguments
       integer(c_int) function nkv_arnoldi_factorization(L, w, Q, mstart, mend, H, ldh, f, scratch, ws, matvec, &
             mv_user, allreduce, ar_user, flags, stream) bind(C, name="nkv_arnoldi_factorization")
