@@ -196,6 +196,68 @@ def test_config3_full_size_hessenberg_vs_oracle(gpu):
         del Q
 
 
+def test_config3_full_size_last_steps_vs_oracle(gpu):
+    """BASELINE size N=100,014,464, m=128: the LAST Arnoldi steps of the device's DCGS2 factorisation
+    against the reference-order MGS2 oracle at the same full size.  Given the device's own final
+    basis q_1..q_j (streamed to the host one column at a time: MGS2 needs only q_i and f, so 1.6 GB
+    of host memory instead of the 103 GB basis), the oracle's update_hessenberg_matrix sequence
+    (krylov_decomposition.f90:155-186: copy -> dot -> cmult -> sub2 per column, twice, then
+    k_normalize; the C oracle's primitives) on f = A q_j gives H(:, j) and q_{j+1}: they match the
+    device's to 1e-11 of max|H| and 1e-10, for j = 64 and j = 128 (the headline's last step)."""
+    lay = box3d_layout(44176)
+    m = 128
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=m + 1)
+    d, _ = syn.laplacian_shift_invert(lay)
+    op = DiagOperator(ctx, d)
+    L = olayout(lay)
+    dref = syn.to_reference_order(lay, d)
+    del d
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    Q = ctx.basis(m + 1)
+    from nekstab_next_amd.krylov_schur import prepare_seed
+    prepare_seed(seed, Q[0])
+    Hd = HessenbergDev(ctx, m)
+    arnoldi_factorization(ctx, op, Q, Hd, 1, m, mode="dcgs2")
+    H = Hd.download()
+    hmax = np.max(np.abs(H))
+    idx = torch.cat([torch.arange(s_, s_ + n, device=ctx.device) for _, s_, n in lay.field_slices()]
+                    + [torch.tensor([lay.time_offset], device=ctx.device)])
+
+    pinned = torch.empty(L.len, dtype=torch.float64, pin_memory=True)
+    gathered = torch.empty(L.len, dtype=torch.float64, device=ctx.device)
+
+    def column(i):   # reference order [vx|vy|vz|t|pr|time] of device column i, gathered on the GPU
+        torch.index_select(Q.storage[i], 0, idx, out=gathered)
+        pinned.copy_(gathered)
+        return pinned.numpy()   # reused buffer: consumed before the next call
+
+    lib, Lp = orc.lib(), ctypes.byref(L.c)
+    orc.set_threads(16)
+    try:
+        for j in (64, m):
+            f = np.empty(L.len)
+            lib.orc_op_diag(Lp, dref, column(j - 1), f, 0.0)        # f = A q_j
+            torch.cuda.synchronize()
+            hcol = np.zeros(j + 1)
+            for _pass in range(2):                                  # :155-168, :171-180
+                for i in range(j):
+                    wrk = column(i)                                 # k_copy(wrk, q_i)
+                    alpha = lib.orc_k_dot(Lp, w, f, wrk)
+                    lib.orc_k_cmult(Lp, wrk, alpha)
+                    lib.orc_k_sub2(Lp, f, wrk)
+                    hcol[i] += alpha
+            alpha = float(np.sqrt(lib.orc_k_dot(Lp, w, f, f)))     # k_normalize :183-186
+            lib.orc_k_cmult(Lp, f, 1.0 / alpha)
+            hcol[j] = alpha
+            err = np.max(np.abs(H[: j + 1, j - 1] - hcol))
+            assert err <= 1e-11 * hmax, (j, err, hmax)
+            np.testing.assert_allclose(column(j)[: L.n].copy(), f[: L.n], rtol=0, atol=1e-10)
+    finally:
+        orc.set_threads(1)
+
+
 @pytest.mark.parametrize("E,mode", [(1996, "cgs2"), (22728, "cgs2"), (1996, "cgs2-native"), (1996, "dcgs2"),
                                     (22728, "dcgs2"), (1996, "dcgs2-native")])
 def test_config4_gmres_vs_oracle(gpu, E, mode):

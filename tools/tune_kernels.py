@@ -113,6 +113,7 @@ VARIANTS = {
     "st_g1024": {"NKV_STREAM_G": 1024},
     "st_g768": {"NKV_STREAM_G": 768},
     "dc_g896": {"NKV_DC_G": 896},
+    "dc_g1536": {"NKV_DC_G": 1536},
     "dl_u4": {"NKV_DL_U": 4},
     "dl_u1": {"NKV_DL_U": 1},
     "dl_g1024": {"NKV_DC_G": 1024},
