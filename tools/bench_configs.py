@@ -3,7 +3,8 @@
 
 config 2: cylinder layout scaled to E=22,728 (N=2,000,064), rotation-scaling operator with
           conjugate pairs, Krylov–Schur k_dim=64, schur_tgt=2 — eager launches vs HIP-graph replay.
-config 4: Newton–Krylov GMRES on J = D - I, cylinder mesh (N=175,648), k_dim=200, tol 1e-9.
+config 4: Newton–Krylov GMRES on J = D - I, cylinder mesh (N=175,648) and N=2,000,064, k_dim=200,
+          tol 1e-9, DCGS2 (default) and CGS2 inner Arnoldi.
 config 5: direct + adjoint Krylov–Schur, N=50,007,232, k_dim=96, two bases resident, + bi-orthogonalisation.
 Prints one JSON object per measurement.
 """
@@ -111,13 +112,13 @@ def main():
         op4 = ShiftedOperator(DiagOperator(ctx4, d), -1.0)
         rhs, sol = ctx4.vector(), ctx4.vector()
         rhs.fill_hash(3)
-        for _ in range(2):
+        for mode in ("dcgs2", "cgs2", "dcgs2", "cgs2"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            info = ts_gmres(ctx4, op4, rhs, sol, GmresConfig(k_dim=200, maxiter=10, tol=1e-9))
+            info = ts_gmres(ctx4, op4, rhs, sol, GmresConfig(k_dim=200, maxiter=10, tol=1e-9, mode=mode))
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps(dict(config="config4", N=lay4.N, seconds=round(dt, 4), matvecs=info.matvecs,
+            print(json.dumps(dict(config="config4", N=lay4.N, mode=mode, seconds=round(dt, 4), matvecs=info.matvecs,
                                   restarts=info.restarts, final_beta2=info.outer_residuals[-1])), flush=True)
     del ctx4, op4, rhs, sol
 
