@@ -402,6 +402,10 @@ def _run_next(world_rank_pair, out, port, tmpdir):
         probe.fill_hash(4)
         info = ts_gmres(ctx2, op, rhs, sol, GmresConfig(k_dim=12, maxiter=20, tol=1e-14, mode="dcgs2"))
         res["gmres"] = (info.inner_residuals, info.outer_residuals, ctx2.dot(sol, probe, False))
+        sol_n = ctx2.vector()   # the one-call library cycle, its all-reduce through the callback
+        info_n = ts_gmres(ctx2, op, rhs, sol_n, GmresConfig(k_dim=12, maxiter=20, tol=1e-14, mode="dcgs2-native"))
+        res["gmres_native_equal"] = (info_n.inner_residuals == info.inner_residuals
+                                     and bool(torch.equal(sol_n.storage, sol.storage)))
 
         lay3 = box3d_layout(23).shard(rank, world)
         ctx3 = NekContext(lay3, weights=syn.mass_weights(lay3), comm=comm, max_cols=32)
@@ -429,10 +433,12 @@ def _run_next(world_rank_pair, out, port, tmpdir):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
-    """svds on delayed re-orthogonalisation, GMRES on DCGS2 and the wave-maker (multi-file mode sets
-    written and read by every rank) on `world` gloo ranks sharing the GPU reproduce the one-rank run:
+    """svds on delayed re-orthogonalisation, GMRES on DCGS2 (Python-driven and the one-call
+    nkv_gmres_dcgs2, identical bit for bit on every rank) and the wave-maker (multi-file mode sets
+    written and read by every rank) on `world` gloo ranks sharing the GPU (4: config 5's split)
+    reproduce the one-rank run:
     singular values and C to 1e-12, GMRES histories 1e-8 (the oracle tests' gate) and the solution's projection 1e-12, the
     modulus of <a, d>_W and the assembled wave-maker field to 1e-12."""
     mgr = mp.Manager()
@@ -462,6 +468,7 @@ def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
         np.testing.assert_allclose(i2, i1, rtol=1e-8)   # as the oracle gate: partial-sum grouping only
         np.testing.assert_allclose(o2, o1, rtol=1e-8)
         assert abs(p2 - p1) <= 1e-12 * abs(p1)
+        assert got["gmres_native_equal"]   # nkv_gmres_dcgs2 == the Python-driven cycle, bit for bit
         ip1, g1 = one["wm"]
         ip2, g2 = got["wm"]
         # the eigenvectors' free phase (dgeev's sign) may differ between world sizes: |<a, d>| and the
