@@ -35,6 +35,7 @@ def test_bench_json_contract(gpu):
     assert cb["cores"] == cb["host"]["threads"] and cb["seconds_per_factorisation_N1e8"] > 0
     assert cb["value_reference_executed_gbs"] > cb["value"]
     assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
+    assert len(d["devices"]) == 1 and d["devices"][0]["pci"] and d["distinct_devices"] is True
     ks = d["krylov_schur_leg"]
     assert ks["schur_cnt"] >= 1 and ks["converged"] >= 4 and ks["ritz_rel_err_vs_exact"] < 1e-10
     assert d["ritz_top8_rel_err"] < 1e-10
@@ -57,6 +58,8 @@ def test_bench_plain_command_two_gloo_ranks_one_gpu(gpu):
         outs[n] = json.loads(lines[0])
     d2 = outs[2]
     assert d2["n_gpus"] == 2 and d2["world"] == 2 and d2["backend"] == "gloo"
+    # both ranks drove the one GPU: the line says so (an 8-GPU RCCL line must say true)
+    assert len(d2["devices"]) == 2 and d2["distinct_devices"] is False
     g = d2["gram_schmidt"]
     assert g["allreduces_per_factorisation"] >= 48 and g["allreduce_ms_per_factorisation_max_over_ranks"] > 0
     assert g["gs_ms_per_factorisation_min_over_ranks"] <= g["gs_ms_per_factorisation_max_over_ranks"]
