@@ -19,6 +19,12 @@ Provenance, per fixture:
   §3), so these are oracle outputs, not reference outputs: they freeze the oracle (a change to it
   shows up as a fixture mismatch) and let the GPU tests check the HIP path without running the
   oracle.  Parity against the reference itself stays "unpinned" (DESIGN.md §3).
+* ``wavemaker_cyl.npz`` — the oracle's ``wave_maker`` (core/sensitivity.f90:3-77: bi-orthogonalise,
+  then sqrt(sum dRe^2 + dIm^2) sqrt(sum aRe^2 + aIm^2)) on the real cylinder mesh (E=1996, 2-D):
+  the direct mode's real part is the reference's own base flow (U, V of ``BF_1cyl0.f00001``, from
+  ``bf_1cyl0_seed.npz``), the other three parts hashed (``synthetic.hash_vector`` seeds 41-43).
+  Oracle output: freezes the restatement and lets the GPU test run the product's file chain
+  against it without the oracle.
 * ``ordering.npz`` — inputs/outputs of the C transliteration of ``quicksort2``
   (core/utils.f90:29-138), ``select_eigenvalues`` (core/eigensolvers.f90:688-754) and
   ``sort_eigendecomp`` (core/lapack_wrapper.f90:181-228), including the pivot defect.
@@ -172,6 +178,35 @@ def gen_solvers():
     orc.set_threads(1)
 
 
+def wavemaker_inputs():
+    """(velocity layout, weights, [dRe, dIm, aRe, aIm] in reference order incl. the time slot)."""
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import cylinder_layout
+    from nekstab_next_amd.sensitivity import velocity_layout
+
+    vlay = velocity_layout(cylinder_layout(1996))
+    nvel = vlay.ldim * vlay.n_v
+    bf = np.load(os.path.join(HERE, "bf_1cyl0_seed.npz"))["seed_ref"]
+    vecs = [np.concatenate([bf[:nvel], [0.0]])]
+    for s_ in (41, 42, 43):
+        vecs.append(syn.to_reference_order(vlay, syn.hash_vector(vlay, s_)))
+    vecs[1] = 0.3 * vecs[1]
+    return vlay, syn.mass_weights(vlay), vecs
+
+
+def gen_wavemaker():
+    import oracle as orc
+
+    vlay, w, vecs = wavemaker_inputs()
+    L = orc.OLayout(vlay.n_v, 0, vlay.ldim, False, vlay.ldim)
+    wm, out = orc.wave_maker(L, w, *vecs)
+    ip = lambda p, q: orc.k_dot(L, w, p, q)  # noqa: E731
+    d, di, a, ai = out
+    np.savez_compressed(os.path.join(HERE, "wavemaker_cyl.npz"), wavemaker=wm,
+                        ad_after=np.array([ip(a, d) + ip(ai, di), ip(a, di) - ip(ai, d)]),
+                        inputs_checksum=np.array([_checksum(v) for v in vecs]))
+
+
 def gen_ordering():
     import oracle as orc
 
@@ -214,8 +249,12 @@ def gen_ordering():
 
 
 if __name__ == "__main__":
+    if "--only-wavemaker" in sys.argv:   # needs only the committed bf_1cyl0_seed.npz, not /root/reference
+        gen_wavemaker()
+        sys.exit(0)
     gen_fld()
     gen_ordering()
     gen_solvers()
+    gen_wavemaker()
     for n in sorted(os.listdir(HERE)):
         print(f"{os.path.getsize(os.path.join(HERE, n)):10d}  {n}")

@@ -120,3 +120,32 @@ def test_golden_config4_gmres(gpu):
     np.testing.assert_allclose(info.inner_residuals[:20], z["inner"][:20], rtol=1e-8)
     got = syn.to_reference_order(lay, sol.to_packed())
     np.testing.assert_allclose(got[:256], z["sol_head"], rtol=1e-9, atol=1e-12)
+
+
+def test_golden_wavemaker_reference_base_flow(gpu, tmp_path):
+    """The product's wave_maker file chain against the frozen oracle output: the four mode parts
+    (the direct mode's real part is the reference's cylinder base flow BF_1cyl0, the rest hashed)
+    written as dRe/dIm<session>0.f00001 and aRe/aIm<session>0.f00002, read back, bi-orthogonalised
+    and combined on the device — to 1e-12 of the field's maximum."""
+    from nekstab_next_amd import fld
+    from nekstab_next_amd.sensitivity import velocity_layout, wave_maker
+
+    z = _load("wavemaker_cyl.npz")
+    vlay = velocity_layout(cylinder_layout(1996))
+    w = syn.mass_weights(vlay)
+    ctx = NekContext(vlay, weights=w, max_cols=4)
+    nvel = vlay.ldim * vlay.n_v
+    bf = _load("bf_1cyl0_seed.npz")["seed_ref"]
+    parts = [np.concatenate([bf[:nvel], [0.0]])]
+    for s_ in (41, 42, 43):
+        parts.append(syn.to_reference_order(vlay, syn.hash_vector(vlay, s_)))
+    parts[1] = 0.3 * parts[1]
+    for (prefix, num), ref in zip((("dRe", 1), ("dIm", 1), ("aRe", 2), ("aIm", 2)), parts):
+        f = fld.fld_from_vector(vlay, syn.from_reference_order(vlay, ref), time=float(num), istep=num)
+        fld.write_fld(str(tmp_path / fld.fld_name(prefix, "cyl", 0, num)), f)
+    res = wave_maker(ctx, str(tmp_path), session="cyl")
+    wm = z["wavemaker"]
+    assert np.max(np.abs(res["wavemaker"] - wm)) <= 1e-12 * np.max(np.abs(wm))
+    d, di, a, ai = res["vectors"]
+    re = ctx.dot(a, d, False) + ctx.dot(ai, di, False)
+    assert abs(re - z["ad_after"][0]) < 1e-12
