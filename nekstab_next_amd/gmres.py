@@ -179,6 +179,9 @@ def dcgs2_cycle(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: 
     by the solution update and is left unfinished.  Returns the number of columns k."""
     from .arnoldi import _dcgs2_step
 
+    if ks > ctx.max_cols or Q.k < ks + 1 or Hd.k < ks:   # the closing multi-dot takes ks + 1 columns
+        raise ValueError(f"GMRES k_dim={ks} needs max_cols >= {ks} (context has {ctx.max_cols}), "
+                         f"a basis of {ks + 1} columns and H of {ks}")
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     nrm2 = ctx.scal[5:6]
     k_used = ks
@@ -208,6 +211,8 @@ def gmres_cycle_native(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVecto
 
     from .arnoldi import _allreduce_callback, _native_scratch
 
+    if ks > ctx.max_cols or Q.k < ks + 1 or Hd.k < ks:   # ws holds the partials of ks + 1 columns
+        raise ValueError(f"GMRES k_dim={ks} needs max_cols >= {ks} (context has {ctx.max_cols})")
     scratch = _native_scratch(ctx, ks)
     base, ld8, fptr = Q.ptr, 8 * ctx.layout.ld, f.ptr
     errors = []

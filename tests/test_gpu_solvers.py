@@ -617,3 +617,16 @@ def test_gmres_native_cycle_is_bit_identical(gpu):
     np.testing.assert_array_equal(a[2], b[2])
     for ya, yb in zip(a[3], b[3]):
         np.testing.assert_array_equal(ya, yb)
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "dcgs2-native"])
+def test_gmres_refuses_a_context_too_small(gpu, mode):
+    """The DCGS2 cycle's closing multi-dot takes k_dim + 1 columns: a context whose workspace holds
+    fewer partials is refused before any launch (no out-of-bounds device writes)."""
+    lay = cylinder_layout(20)
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), max_cols=8)
+    op = DiagOperator(ctx, syn.diag_spectrum(lay)[0])
+    rhs, sol = ctx.vector(), ctx.vector()
+    rhs.fill_hash(3)
+    with pytest.raises(ValueError, match="max_cols"):
+        ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=12, maxiter=1, mode=mode))
