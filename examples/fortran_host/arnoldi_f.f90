@@ -1,7 +1,10 @@
 ! arnoldi_f.f90 — a Fortran host (the reference's language) running DCGS2 Arnoldi through the C ABI:
 ! the replacement of arnoldi_factorization / update_hessenberg_matrix (krylov_decomposition.f90)
 ! by the loop of INTEGRATION.md §2b on one rank (gop = identity), then W-orthonormality and the
-! Arnoldi relation A Q_m = Q_{m+1} H checked through the same calls.   usage: arnoldi_f [E [m]]
+! Arnoldi relation A Q_m = Q_{m+1} H checked through the same calls; then ts_gmres
+! (newton_krylov.f90:241-294) with its inner loop as ONE library call (nkv_gmres_dcgs2): restarts,
+! the small least-squares problem on the host (Givens + back substitution here; the reference's
+! lstsq/dgels in nekStab), x += Q y with nkv_combine.   usage: arnoldi_f [E [m]]
 module diag_callback
    ! the operator handed to nkv_arnoldi_dcgs2 as a callback: y = d .* x on the library's stream
    use iso_c_binding
@@ -31,6 +34,7 @@ program arnoldi_f
    real(c_double), allocatable, target :: hw(:), H(:, :), g(:), dh(:)
    real(c_double), target :: r2
    real(c_double) :: orth, arn, hmax
+   logical :: gm_ok
 
    E = 512; m = 24
    nargs = command_argument_count()
@@ -138,10 +142,69 @@ program arnoldi_f
    else
       print '(a)', 'arnoldi_f: nkv_arnoldi_dcgs2 DIFFERS from the step-by-step loop'
    end if
-   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12 .and. same) then
+   call gmres_leg(gm_ok)
+   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12 .and. same .and. gm_ok) then
       print '(a)', 'arnoldi_f: OK'
    else
       print '(a)', 'arnoldi_f: FAILED'
       stop 1
    end if
+contains
+
+   subroutine gmres_leg(ok)
+      ! ts_gmres: Q(:,1) = r/||r||; inner loop = nkv_gmres_dcgs2; y = argmin ||beta e1 - H y||;
+      ! x += Q y; r = b - A x (initialize_gmres_vector); 3 restarts of m columns
+      logical, intent(out) :: ok
+      type(c_ptr) :: b, x, dq, rv, yd, Qg, Hg
+      real(c_double), allocatable, target :: Hh(:, :), res(:), y(:), cs(:), sn(:), gv(:), Rm(:, :)
+      real(c_double), target :: bb
+      real(c_double) :: beta, bnorm, lsres, v, last_res
+      integer(c_int), target :: k
+      integer :: it, cc, rr
+      call ck(hipMalloc(b, vbytes), 'b'); call ck(hipMalloc(x, vbytes), 'x')
+      call ck(hipMalloc(dq, vbytes), 'dq'); call ck(hipMalloc(rv, vbytes), 'r')
+      call ck(hipMalloc(yd, int(m, c_size_t)*8), 'yd')
+      call ck(hipMalloc(Qg, (m + 1)*vbytes), 'Qg'); call ck(hipMalloc(Hg, int(m*(m + 1), c_size_t)*8), 'Hg')
+      call ck(hipMemset(b, 0, vbytes), 'b0'); call ck(hipMemset(x, 0, vbytes), 'x0')
+      call ck(hipMemset(Qg, 0, (m + 1)*vbytes), 'Q0')
+      allocate (Hh(m + 1, m), res(m), y(m), cs(m + 2), sn(m + 2), gv(m + 2), Rm(m + 2, m))
+      call ck(nkv_fill_hash(L, b, 3_c_int64_t, 0_c_int64_t, 0_c_int64_t, st), 'rhs')
+      call ck(nkv_copy(L, rv, b, NKV_TIME, st), 'r = b')                        ! x = 0: r = b
+      call ck(nkv_dot(L, w, b, b, nrm, ws, 0, st), 'rhs norm')
+      call ck(hipMemcpy(c_loc(bb), nrm, 8_c_size_t, hipMemcpyDeviceToHost), 'bb')
+      bnorm = sqrt(bb); beta = bnorm
+      Lcb = L; dcb = d
+      do it = 1, 3
+         call ck(nkv_copy(L, Qg, rv, NKV_TIME, st), 'Q(1) = r')
+         call ck(nkv_dot(L, w, Qg, Qg, nrm, ws, 0, st), 'r norm')
+         call ck(nkv_normalize_dev(L, Qg, nrm, c_null_ptr, 0, st), 'Q(1) = r/|r|')
+         call ck(hipMemset(Hg, 0, int(m*(m + 1), c_size_t)*8), 'H0')
+         call ck(nkv_gmres_dcgs2(L, w, Qg, int(m, c_int), beta, 1.0d-30, Hg, int(m + 1, c_int64_t), f, scr, ws, &
+                                 c_funloc(diag_mv), c_null_ptr, c_null_funptr, c_null_ptr, res, k, 0, st), 'gmres')
+         call ck(hipMemcpy(c_loc(Hh), Hg, int(m*(m + 1), c_size_t)*8, hipMemcpyDeviceToHost), 'H down')
+         cs = 0; sn = 0; gv = 0; gv(1) = beta; Rm = 0
+         do cc = 1, k
+            Rm(1:cc + 1, cc) = Hh(1:cc + 1, cc)
+            lsres = nkv_givens_column(int(cc - 1, c_int), Rm(1, cc), cs, sn, gv)
+         end do
+         do rr = k, 1, -1
+            v = gv(rr)
+            do cc = rr + 1, k
+               v = v - Rm(rr, cc)*y(cc)
+            end do
+            y(rr) = v/Rm(rr, rr)
+         end do
+         call ck(hipMemcpy(yd, c_loc(y), int(k, c_size_t)*8, hipMemcpyHostToDevice), 'y up')
+         call ck(nkv_combine(L, Qg, k, yd, dq, NKV_TIME, st), 'dq = Q y')             ! k_matmul
+         call ck(nkv_axpby(L, x, 1.0d0, dq, 1.0d0, NKV_TIME, st), 'x += dq')         ! k_add2
+         call ck(nkv_op_diag(L, d, x, rv, 0.0d0, st), 'A x')                          ! initialize_gmres_vector
+         call ck(nkv_axpby(L, rv, -1.0d0, b, 1.0d0, NKV_TIME, st), 'r = b - A x')
+         call ck(nkv_dot(L, w, rv, rv, nrm, ws, 0, st), 'residual')
+         call ck(hipMemcpy(c_loc(bb), nrm, 8_c_size_t, hipMemcpyDeviceToHost), 'res down')
+         last_res = res(k); beta = sqrt(bb)
+         print '(a,i0,a,i0,a,es10.3,a,es10.3,a,es10.3)', 'arnoldi_f: gmres restart ', it, ': ', k, &
+            ' columns, reported ', last_res, ', least-squares ', lsres, ', ||b - A x||_W ', beta
+      end do
+      ok = abs(beta - lsres) <= 1.0d-10*bnorm .and. beta < 1.0d-6*bnorm
+   end subroutine gmres_leg
 end program arnoldi_f

@@ -56,6 +56,30 @@ module nkv_bindings
          type(c_ptr), value :: x, nrm2, beta, stream
          integer(c_int), value :: flags
       end function
+      integer(c_int) function nkv_copy(L, dst, src, flags, stream) bind(C, name="nkv_copy")
+         import :: c_int, c_ptr, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: dst, src, stream
+         integer(c_int), value :: flags
+      end function
+      integer(c_int) function nkv_axpby(L, x, a, y, b, flags, stream) bind(C, name="nkv_axpby")
+         import :: c_int, c_ptr, c_double, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: x, y, stream
+         real(c_double), value :: a, b
+         integer(c_int), value :: flags
+      end function
+      integer(c_int) function nkv_combine(L, Q, k, y, out, flags, stream) bind(C, name="nkv_combine")
+         import :: c_int, c_ptr, nkv_layout
+         type(nkv_layout), intent(in) :: L
+         type(c_ptr), value :: Q, y, out, stream
+         integer(c_int), value :: k, flags
+      end function
+      real(c_double) function nkv_givens_column(k, h, cs, sn, g) bind(C, name="nkv_givens_column")
+         import :: c_int, c_double
+         integer(c_int), value :: k
+         real(c_double), intent(inout) :: h(*), cs(*), sn(*), g(*)
+      end function
       integer(c_int) function nkv_block_dot(L, w, Q, j, f, h, ws, flags, stream) bind(C, name="nkv_block_dot")
          import :: c_int, c_ptr, nkv_layout
          type(nkv_layout), intent(in) :: L
