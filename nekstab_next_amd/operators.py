@@ -13,6 +13,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ._lib import NKV_TIME
 from .vector import NekContext, NekVector
 
 
@@ -135,6 +136,95 @@ class CallableOperator(LinearOperator):
         if self._rmv is None:
             raise NotImplementedError("operator has no adjoint")
         self._rmv(x, y)
+
+
+class LegacyMatvec(LinearOperator):
+    """The legacy ``matvec(f, q)`` dispatcher (core/matvec.f90:56-146): ``uparam(1) = mode``
+    selects the map applied to q, in the reference's order and with its ``k_*`` time handling
+    (k_sub2 / k_cmult / k_add2 update ``time``, krylov_subspace.f90:94-127).  ``op.matvec`` is the
+    forward linearised map, ``op.rmatvec`` the adjoint map; ``fd_op.matvec`` (optional) the
+    finite-difference forward map used when ``iffindiff`` (:113-118, :536-541).
+
+    ============  =======  =======================================================================
+    mode          evop     f =
+    ============  =======  =======================================================================
+    [3.0, 3.2)    ``d``    forward map (or FD map) of q                                   (:111-119)
+    [3.2, 3.3)    ``a``    adjoint map of q                                               (:122-125)
+    [3.3, 3.4)    ``p``    adjoint(forward(q)), transient_growth_map                 (:128-131, :478-495)
+    4.x           —        -(adjoint(q) - q), ts_force_sensitivity_map               (:134-136, :499-516)
+    2.x           ``n``    forward(q) - q, newton_linearized_map                     (:139-143, :520-571)
+    ============  =======  =======================================================================
+
+    Mode 2.1 (Newton for a periodic orbit, :550-563) borders the map with the period row:
+    f += b_fc * q%time and f%time = k_dot(b_ic, q); other 2.x modes set f%time = 0.  ``b_fc`` /
+    ``b_ic`` are the time derivatives compute_bvec produces (:575-613, one Nek step — out of scope
+    here, so the caller supplies them); they are copied with time = 0 as compute_bvec leaves them
+    (:610).  The reference silently leaves f untouched for a mode that selects nothing; here that
+    is refused at construction.  No host synchronisation: q%time and the period dot stay on the
+    device."""
+
+    def __init__(self, mode: float, op: LinearOperator, fd_op: LinearOperator | None = None,
+                 b_fc: NekVector | None = None, b_ic: NekVector | None = None):
+        mode = float(mode)
+        fl = int(np.floor(mode))
+        if 3.0 <= mode < 3.2:
+            self.evop = "d"
+        elif 3.2 <= mode < 3.3:
+            self.evop = "a"
+        elif 3.3 <= mode < 3.4:
+            self.evop = "p"
+        elif fl == 4:
+            self.evop = None
+        elif fl == 2:
+            self.evop = "n"
+        else:
+            raise ValueError(f"uparam(1)={mode} selects no map (core/matvec.f90:110-143)")
+        self.mode, self.op, self.fd_op = mode, op, fd_op
+        self.upo = mode == 2.1
+        self._wrk = None
+        self._t = None
+        if self.upo:
+            if b_fc is None or b_ic is None:
+                raise ValueError("uparam(1)=2.1 needs b_fc and b_ic (compute_bvec, core/matvec.f90:555-560)")
+            ctx = b_fc.ctx
+            self.b_fc, self.b_ic = ctx.vector(), ctx.vector()
+            for dst, src in ((self.b_fc, b_fc), (self.b_ic, b_ic)):
+                dst.copy_from(src, time=False)
+            self._t = torch.zeros(1, dtype=torch.float64, device=ctx.device)
+
+    def _forward(self, q: NekVector, f: NekVector) -> None:
+        (self.fd_op if self.fd_op is not None else self.op).matvec(q, f)
+
+    def matvec(self, q: NekVector, f: NekVector) -> None:
+        from .vector import k_cmult, k_sub2
+
+        ctx = q.ctx
+        m, fl = self.mode, int(np.floor(self.mode))
+        if 3.0 <= m < 3.2:
+            self._forward(q, f)
+        elif 3.2 <= m < 3.3:
+            self.op.rmatvec(q, f)
+        elif 3.3 <= m < 3.4:
+            if self._wrk is None:
+                self._wrk = ctx.vector()
+            self.op.matvec(q, self._wrk)
+            self.op.rmatvec(self._wrk, f)
+        elif fl == 4:
+            self.op.rmatvec(q, f)
+            k_sub2(f, q)
+            k_cmult(f, -1.0)
+        else:
+            self._forward(q, f)
+            k_sub2(f, q)
+            lay = ctx.layout
+            tslot = f.storage[lay.time_offset:lay.time_offset + 1]
+            if self.upo:
+                q_time = q.ptr + 8 * lay.time_offset
+                ctx.call("nkv_axpy_dev", f.ptr, q_time, 1.0, self.b_fc.ptr, NKV_TIME, ctx.stream)
+                ctx.dot_dev(self.b_ic, q, self._t, time=ctx.time_in_dot)
+                tslot.copy_(self._t)
+            else:
+                tslot.zero_()
 
 
 class ComplexDiagOperator(LinearOperator):

@@ -425,6 +425,46 @@ def ts_gmres(L: OLayout, w, matvec, rhs, maxiter, ksize, tol, findiff=False):
     return sol, hist
 
 
+def legacy_matvec(L: OLayout, w, mode, fwd, adj, f, q, fd=None, b_fc=None, b_ic=None):
+    """The legacy dispatcher ``matvec(f, q)`` on ``uparam(1) = mode`` (matvec.f90:56-146) over
+    reference-order vectors; ``fwd`` / ``adj`` / ``fd`` are the forward, adjoint and finite-difference
+    maps ``m(x, y)``.  Returns evop.  Mode 2.x is newton_linearized_map (:520-571): f = Phi'(q) - q
+    (k_sub2, time included), and for 2.1 (the UPO period row) f += b_fc * q%time, then
+    f%time = k_dot(b_ic, q) — compute_bvec's vectors carry time = 0 (:610); otherwise f%time = 0."""
+    c = ctypes.byref(L.c)
+    fwd_or_fd = fd if fd is not None else fwd
+    if 3.0 <= mode < 3.2:
+        fwd_or_fd(q, f)
+        return "d"
+    if 3.2 <= mode < 3.3:
+        adj(q, f)
+        return "a"
+    if 3.3 <= mode < 3.4:       # transient_growth_map :478-495
+        wrk = L.zeros()
+        fwd(q, wrk)
+        adj(wrk, f)
+        return "p"
+    if int(np.floor(mode)) == 4:  # ts_force_sensitivity_map :499-516
+        adj(q, f)
+        lib().orc_k_sub2(c, f, q)
+        lib().orc_k_cmult(c, f, -1.0)
+        return None
+    if int(np.floor(mode)) == 2:
+        fwd_or_fd(q, f)
+        lib().orc_k_sub2(c, f, q)
+        if mode == 2.1:
+            bvec = b_fc * q[-1]
+            bvec[-1] = 0.0
+            lib().orc_k_add2(c, f, np.ascontiguousarray(bvec))
+            bic = np.array(b_ic, dtype=np.float64)
+            bic[-1] = 0.0
+            f[-1] = k_dot(L, w, bic, q)
+        else:
+            f[-1] = 0.0
+        return "n"
+    raise ValueError(f"uparam(1)={mode} selects no map")
+
+
 def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):
     """sensitivity.f90:393-469.  Inputs are modified copies; returns (dRe, dIm, aRe, aIm).
 

@@ -163,3 +163,34 @@ def test_k_dot_time_component():
     L2 = orc.OLayout(100, 20, 2, time_in_dot=False)
     assert orc.k_dot(L2, w, p, q) == 0.0
     assert orc.real_dot(L2, w, p, q) == 6.0  # real_dot always includes time (nek_vectors.f90:106)
+
+
+def test_legacy_matvec_closed_forms():
+    """oracle.legacy_matvec (matvec.f90:56-146) on a diagonal map D (self-adjoint) in closed form:
+    3.x -> D q, 3.3 -> D^2 q, 4.x -> q - D q (time: q%time - 0), 2.0 -> D q - q with time 0, 2.1 ->
+    D q - q + b_fc q%time with time = <b_ic, q>_W (the time of b_ic ignored, compute_bvec :610)."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=40)
+    L = olayout(lay, time_in_dot=True)
+    w = syn.mass_weights(lay)
+    d = syn.to_reference_order(lay, syn.diag_spectrum(lay)[0])
+    mv = oracle_diag_matvec(L, d)
+    rng = np.random.default_rng(0)
+    q = rng.standard_normal(L.len)
+    bfc, bic = rng.standard_normal(L.len), rng.standard_normal(L.len)
+    n = L.n
+    for mode, evop, fields, time in (
+            (3.1, "d", d[:n] * q[:n], 0.0),
+            (3.2, "a", d[:n] * q[:n], 0.0),
+            (3.3, "p", d[:n] * d[:n] * q[:n], 0.0),
+            (4.1, None, q[:n] - d[:n] * q[:n], q[-1]),
+            (2.0, "n", d[:n] * q[:n] - q[:n], 0.0),
+            (2.1, "n", d[:n] * q[:n] - q[:n] + bfc[:n] * q[-1], None)):
+        f = np.full(L.len, 7.0)
+        assert orc.legacy_matvec(L, w, mode, mv, mv, f, q.copy(), b_fc=bfc, b_ic=bic) == evop
+        np.testing.assert_allclose(f[:n], fields, rtol=0, atol=1e-15)
+        if time is None:
+            wf = np.concatenate([np.tile(w, L.nwf), np.zeros(L.np)])
+            time = float(np.sum(wf * bic[:n] * q[:n]))
+        assert abs(f[-1] - time) <= 1e-12 * max(1.0, abs(time))
+    with pytest.raises(ValueError):
+        orc.legacy_matvec(L, w, 3.4, mv, mv, np.zeros(L.len), q)
