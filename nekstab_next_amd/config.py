@@ -15,7 +15,8 @@ class KrylovSchurConfig:
     #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order);
     #                           "dcgs2-native" | "cgs2-native" | "mgs2-native": the same sequences driven
     #                           by the library's one-call entry points (bit-identical)
-    seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "as_is"
+    seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "load" (a
+    #                                krylov_schur.load_seed vector; both eigensolvers.f90:192-223) | "as_is"
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
     graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)

@@ -115,6 +115,22 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
     return mstart, selected
 
 
+def load_seed(ctx: NekContext, directory: str, session: str = "nek", transpose: bool = False) -> NekVector:
+    """The ``ifseed_load`` seed (eigensolvers.f90:210-223): the real part of mode 1 of an earlier
+    run, ``dRe<session>0.f00001`` for the direct problem (uparam(1) in [3.0, 3.2)) or
+    ``aRe<session>0.f00001`` for the adjoint ([3.2, 3.3)), read as ``load_fld`` + ``nopcopy`` do
+    (velocity, pressure, scalars; time 0).  Each rank reads its own elements of a multi-file set.
+    Pass it to :func:`krylov_schur` with ``seed_mode="load"``: k_normalize, one matvec,
+    Q(1) = A seed, not renormalised (:222-223)."""
+    from . import fld
+
+    prefix = "aRe" if transpose else "dRe"
+    files = fld.read_fld_set(directory, prefix, session, 1)
+    if not files:
+        raise FileNotFoundError(f"{fld.fld_name(prefix, session, 0, 1)} not found in {directory}")
+    return ctx.vector().from_packed(fld.vector_from_fld(ctx.layout, files))
+
+
 def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: KrylovSchurConfig | None = None,
                  transpose: bool = False, on_restart=None, Q: Basis | None = None, on_step=None,
                  start=None) -> KrylovSchurResult:
@@ -138,9 +154,9 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         pass
     elif cfg.seed_mode == "normalize":
         prepare_seed(seed, Q[0])
-    elif cfg.seed_mode == "noise":
-        # ifseed_nois branch of the in-tree driver: Q(1) = A (seed/||seed||), NOT renormalised
-        # (eigensolvers.f90:195-203)
+    elif cfg.seed_mode in ("noise", "load"):
+        # ifseed_nois / ifseed_load branches of the in-tree driver: Q(1) = A (seed/||seed||), NOT
+        # renormalised (eigensolvers.f90:195-203, 210-223; "load" seeds come from load_seed)
         w2 = ctx.vector()
         w2.copy_from(seed)
         from .vector import k_normalize
@@ -171,7 +187,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # then projects against it as it stands, so its basis is not orthonormal (a projection onto an
     # unnormalised vector removes only part of the component) and classical and modified
     # Gram–Schmidt no longer agree.  That mode therefore runs the reference's own operation order.
-    mode = "mgs2" if (cfg.seed_mode == "noise" and start is None) else cfg.mode
+    mode = "mgs2" if (cfg.seed_mode in ("noise", "load") and start is None) else cfg.mode
     if mode != cfg.mode:
         graphs, lazy = None, False
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)

@@ -446,6 +446,39 @@ def test_krylov_schur_knobs(gpu):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
 
 
+@pytest.mark.parametrize("transpose", [False, True])
+def test_krylov_schur_load_seed_vs_oracle(gpu, tmp_path, transpose):
+    """ifseed_load (eigensolvers.f90:210-223): mode 1's real part of an earlier run, dRe (direct) or
+    aRe (adjoint) <session>0.f00001, written by the oracle's independent #std writer; the product
+    reads it (load_seed), k_normalizes it and applies one matvec (seed_mode "load").  The oracle
+    reads the same file with its own reader and runs the same seed: trajectory and Ritz values
+    against it (1e-10), and the other file is a different vector, so the prefix choice shows."""
+    import nekio
+    from nekstab_next_amd.krylov_schur import load_seed
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=32)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    dref = syn.to_reference_order(lay, d)
+    g = nekio.Geom(lay.ldim, lay.lx1, lay.lx2, lay.nelgv)
+    for prefix, s in (("dRe", 11), ("aRe", 12)):
+        nekio.write_std(str(tmp_path / f"{prefix}cyl0.f00001"), g, syn.to_reference_order(lay, syn.hash_vector(lay, s)))
+    seed = load_seed(ctx, str(tmp_path), "cyl", transpose=transpose)
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="load"),
+                       transpose=transpose)
+    s_ref = nekio.read_std_vector([str(tmp_path / f"{'aRe' if transpose else 'dRe'}cyl0.f00001")], g)
+    np.testing.assert_allclose(syn.to_reference_order(lay, seed.to_packed()), s_ref, rtol=0, atol=1e-13)
+    orc.k_normalize(L, w, s_ref)
+    q1 = np.zeros(L.len)
+    orc.lib().orc_op_diag(ctypes.byref(L.c), dref, s_ref, q1, 0.0)
+    ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
+    _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
+    with pytest.raises(FileNotFoundError):
+        load_seed(ctx, str(tmp_path), "other")
+
+
 @pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-native"])
 @pytest.mark.parametrize("findiff", [False, True])
 def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
