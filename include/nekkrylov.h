@@ -117,6 +117,8 @@ int nkv_sub3(const nkv_layout* L, double* p, const double* q, const double* r, u
 int nkv_axpy_dev(const nkv_layout* L, double* x, const double* alpha_dev, double sign, const double* y,
                  unsigned flags, void* stream);
 /* x <- x / sqrt(*nrm2_dev)   (k_normalize, krylov_subspace.f90:75-92); writes sqrt to beta_dev. */
+/* Every stored row is scaled, the time slot included (flags reserved, pass 0); eigensolvers.f90's
+ * own normalize (nopcmult, :78-116) keeps time — its host restores the slot. */
 int nkv_normalize_dev(const nkv_layout* L, double* x, const double* nrm2_dev, double* beta_dev,
                       unsigned flags, void* stream);
 

@@ -367,7 +367,38 @@ def combine(out: NekVector, Q: Basis, y: torch.Tensor, k: int, with_time: bool =
              NKV_OVERWRITE | (NKV_TIME if with_time else 0), ctx.stream)
 
 
+# ---------------------------------------------------------------------------------------------
+# the in-tree solver's own inner product (core/eigensolvers.f90:3-116): weighted fields only —
+# pressure and time never enter, whatever uparam(1) says.
+# ---------------------------------------------------------------------------------------------
+
+def inner_product(p: NekVector, q: NekVector) -> float:
+    """alpha = sum over vx, vy, [vz], scalars of glsc3(p_f, bm1s, q_f) (eigensolvers.f90:3-56)."""
+    return p.ctx.dot(p, q, time=False)
+
+
+def norm(q: NekVector) -> float:
+    """sqrt(inner_product(q, q)) (eigensolvers.f90:60-74)."""
+    return float(np.sqrt(inner_product(q, q)))
+
+
+def normalize(q: NekVector) -> float:
+    """q <- q / norm(q) by nopcmult: every field incl. pressure, ``time`` untouched
+    (eigensolvers.f90:78-116).  Returns the norm; device-side, one host read for the return."""
+    ctx = q.ctx
+    out = ctx.scal[1:2]
+    ctx.dot_dev(q, q, out, time=False)
+    beta = ctx.scal[2:3]
+    to = ctx.layout.time_offset
+    t_keep = ctx.scal[6:7]
+    t_keep.copy_(q.storage[to:to + 1])          # nkv_normalize_dev scales every row, time included
+    ctx.call("nkv_normalize_dev", q.ptr, _ptr(out), _ptr(beta), 0, ctx.stream)
+    q.storage[to:to + 1].copy_(t_keep)
+    return float(beta.item())
+
+
 __all__ = [
     "NekContext", "NekVector", "ComplexNekVector", "Basis", "k_dot", "k_norm", "k_normalize", "k_cmult",
     "k_add2", "k_sub2", "k_sub3", "k_zero", "k_copy", "k_matmul", "combine", "NKV_NORM2",
+    "inner_product", "norm", "normalize",
 ]

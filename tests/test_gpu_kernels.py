@@ -1100,3 +1100,29 @@ def test_mgs2_step_combine_normalize_store_vs_oracle(gpu, time_dot):
     ctx.call("nkv_normalize_store", out.ptr, nrm2.data_ptr(), qn.ptr, beta.data_ptr(), 0, ctx.stream)
     np.testing.assert_array_equal(qn.to_packed(), out.to_packed() * 0.5)
     assert beta.item() == 2.0
+
+
+@pytest.mark.parametrize("name", ["2d", "3d_scalar"])
+def test_inner_product_norm_normalize_vs_oracle(gpu, name):
+    """The in-tree solver's inner_product / norm / normalize (eigensolvers.f90:3-116): weighted
+    fields only, pressure and time never enter — even on a context with time inside k_dot
+    (uparam(1)==2.1); normalize scales pressure too (nopcmult) and leaves time alone."""
+    from nekstab_next_amd.vector import inner_product, norm, normalize
+
+    lay = LAYOUTS[name]
+    ctx, w = make_ctx(lay, time_in_dot=True)
+    L = olayout(lay, time_in_dot=False)
+    p_h, q_h = syn.hash_vector(lay, 3), syn.hash_vector(lay, 4)
+    p_h[lay.time_offset], q_h[lay.time_offset] = 0.7, -1.3
+    p, q = dev_vec(ctx, p_h), dev_vec(ctx, q_h)
+    pr, qr = syn.to_reference_order(lay, p_h), syn.to_reference_order(lay, q_h)
+    ref = orc.k_dot(L, w, pr, qr)
+    assert abs(inner_product(p, q) - ref) <= 1e-13 * abs(ref)
+    nref = np.sqrt(orc.k_dot(L, w, qr, qr))
+    assert abs(norm(q) - nref) <= 1e-13 * nref
+    a = normalize(q)
+    assert abs(a - nref) <= 1e-13 * nref
+    got = syn.to_reference_order(lay, q.to_packed())
+    np.testing.assert_allclose(got[:-1], qr[:-1] / nref, rtol=1e-14, atol=1e-16)
+    assert got[-1] == -1.3
+    assert abs(inner_product(q, q) - 1.0) < 1e-14
