@@ -2431,8 +2431,11 @@ int nkv_gmres_dcgs2(const nkv_layout* L, const double* w, double* Q, int kmax, d
     double* hd = scratch_dev;                                      // 2(kmax+1)
     double* coef = scratch_dev + 2 * (kmax + 1);                   // 3 kmax + 5
     double* nrm2 = scratch_dev + nkv_arnoldi_scratch_doubles(kmax) - 1;
-    double* host = static_cast<double*>(malloc(sizeof(double) * (size_t)(4 * (kmax + 2))));
-    if (!host) return fail(NKV_EINVAL, "gmres: host allocation failed");
+    // pinned: the per-column H download is a direct DMA (no staging copy) before the residual test
+    double* host = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&host), sizeof(double) * (size_t)(4 * (kmax + 2)),
+                      hipHostMallocDefault) != hipSuccess || !host)
+        return fail(NKV_EHIP, "gmres: pinned host allocation failed");
     double *h = host, *cs = host + (kmax + 2), *sn = cs + (kmax + 2), *g = sn + (kmax + 2);
     for (int i = 0; i < kmax + 2; ++i) g[i] = 0.0;
     g[0] = beta;
@@ -2465,7 +2468,7 @@ int nkv_gmres_dcgs2(const nkv_layout* L, const double* w, double* Q, int kmax, d
         k_used = k;
         if (res * res < tol2) break;
     }
-    free(host);
+    (void)hipHostFree(host);
     if (rc != NKV_OK) return rc;
     *k_out = k_used;
     // close: Q column k_used against Q[0:k_used+1] -> H row k_used corrected, H(k_used, k_used-1) final

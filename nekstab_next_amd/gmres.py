@@ -143,10 +143,11 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
                 info.converged = True
                 break
             continue
+        col = _pinned_column(ks)
         for k in range(1, ks + 1):
             arnoldi_factorization(ctx, op, Q, Hd, k, k, f=f, mode=cfg.mode)
             info.matvecs += 1
-            H[: k + 1, k - 1] = Hd.t[k - 1, : k + 1].cpu().numpy()
+            H[: k + 1, k - 1] = _download(col, Hd.t[k - 1, : k + 1])
             beta = giv.add_column(H[: k + 1, k - 1])        # ||e - H y|| without solving for y
             info.inner_residuals.append(beta ** 2)
             k_used = k
@@ -168,6 +169,19 @@ def ts_gmres(ctx: NekContext, op: LinearOperator, rhs: NekVector, sol: NekVector
     return info
 
 
+def _pinned_column(ks: int) -> torch.Tensor:
+    """Page-locked host buffer for the per-column H download: a direct DMA, no staging copy."""
+    return torch.empty(ks + 1, dtype=torch.float64, pin_memory=True)
+
+
+def _download(buf: torch.Tensor, src: torch.Tensor) -> np.ndarray:
+    """src (a device vector) -> host, through the pinned ``buf``; waits for the stream."""
+    n = src.numel()
+    buf[:n].copy_(src, non_blocking=True)
+    torch.cuda.current_stream(src.device).synchronize()
+    return buf[:n].numpy()
+
+
 def dcgs2_cycle(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: int, giv: GivensResidual,
                 stop) -> int:
     """The inner loop (newton_krylov.f90:250-276) on one continuous DCGS2 factorisation
@@ -184,12 +198,13 @@ def dcgs2_cycle(ctx: NekContext, apply, Q, Hd: HessenbergDev, f: NekVector, ks: 
                          f"a basis of {ks + 1} columns and H of {ks}")
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
     nrm2 = ctx.scal[5:6]
+    col = _pinned_column(ks)
     k_used = ks
     for k in range(1, ks + 1):
         apply(Q[k - 1], f)
         _dcgs2_step(ctx, Q, Hd, k, f, first=(k == 1), nrm2=nrm2)
         Hd.t[k - 1, k].copy_(torch.sqrt(nrm2[0]))            # provisional H(k, k-1), on the device
-        beta = giv.add_column(Hd.t[k - 1, : k + 1].cpu().numpy())
+        beta = giv.add_column(_download(col, Hd.t[k - 1, : k + 1]))
         k_used = k
         if stop(beta):
             break

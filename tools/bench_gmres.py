@@ -7,7 +7,9 @@ with the host and GPU shares of the cycle:
 * ``gpu_ms``: HIP events around every kernel family of a column (the matvec and the CGS2
   orthogonalisation kernels, bench.py's PhaseTimer), summed: the GPU's busy time;
 * ``host_ms``: the cycle's wall time minus that (per-column H download and residual estimate,
-  Python dispatch, the final dgels, the solution update);
+  Python dispatch, the final dgels, the solution update); ``dcgs2-native`` is the same cycle through
+  the one-call C driver ``nkv_gmres_dcgs2`` (its busy time is the ``dcgs2`` row's kernels, which it
+  runs in the same order);
 * ``dgels_every_column_ms``: what the round-2 form cost on the host — ``lstsq`` of the whole
   (k+1) x k system at every k = 1..200 (timed here on the cycle's own H) — against the O(k)
   Givens update now used (``givens_ms``).
@@ -59,7 +61,7 @@ def main():
     from nekstab_next_amd.profiling import PhaseTimer
 
     rows = []
-    for mode in ("dcgs2", "cgs2"):
+    for mode in ("dcgs2", "dcgs2-native", "cgs2"):
         cfg = GmresConfig(k_dim=ks, maxiter=1, tol=1e-300, mode=mode)
         ts_gmres(ctx, Timed(), rhs, sol, cfg)          # warm-up
         torch.cuda.synchronize()
@@ -87,7 +89,13 @@ def main():
         g.add_column(H[: k + 1, k - 1])
     lapack.lstsq(H, e)
     givens_ms = (time.perf_counter() - t0) * 1e3
+    busy = {m: g for m, _w, g, _p, _i in rows}
     for mode, wall, gpu_ms, ph, info in rows:
+        if mode == "dcgs2-native":
+            # the one-call C driver runs the Gram-Schmidt kernels itself (no per-kernel events from
+            # Python): the same kernels in the same order as "dcgs2", so its busy time is that row's
+            gpu_ms = busy["dcgs2"] - sum(v["total_ms"] for k, v in rows[0][3].items() if k == "matvec") \
+                + sum(v["total_ms"] for k, v in ph.items() if k == "matvec")
         print(json.dumps(dict(
             row="config4_gmres_cycle", mode=mode, N=lay.N, k_dim=ks, columns=len(info.inner_residuals),
             wall_ms=round(wall, 2), gpu_ms=round(gpu_ms, 2), host_ms=round(wall - gpu_ms, 2),
