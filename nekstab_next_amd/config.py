@@ -32,5 +32,7 @@ class GmresConfig:
     k_dim: int = 100          # inner Krylov dimension (ksize)
     maxiter: int = 100        # restarts (newton_krylov.f90:120: ts_gmres(f, dq, 100, k_dim, calls))
     tol: float = 1e-9         # max(param(21), param(22)) (newton_krylov.f90:236); test on beta**2
-    mode: str = "dcgs2"       # inner Arnoldi: one continuous DCGS2 factorisation (gmres.py); "cgs2" / "mgs2"
+    mode: str = "dcgs2-native"  # inner Arnoldi: one continuous DCGS2 factorisation, the column loop in the
+    #                             library (nkv_gmres_dcgs2; "dcgs2": the same cycle driven from Python, bit-
+    #                             identical, 7 % slower at config 4); "cgs2" / "mgs2" (gmres.py)
     findiff: bool = False     # iffindiff relaxed exits (1e-8 inner, 1e-6 outer; :269, :292)

@@ -20,7 +20,8 @@ the Arnoldi step before it is read); when the inner loop runs to k_dim without c
 reference leaves ``k = k_dim+1`` and reads ``yvec(k_dim+1)`` out of bounds in ``k_matmul`` — here the
 update uses the k_dim columns that exist.
 
-Orthogonalisation (``GmresConfig.mode``): ``"dcgs2"`` runs the inner Arnoldi as ONE continuous
+Orthogonalisation (``GmresConfig.mode``): ``"dcgs2-native"`` (default) / ``"dcgs2"`` (the same
+sequence driven from Python, bit-identical) runs the inner Arnoldi as ONE continuous
 DCGS2 factorisation (two reads of the basis per column instead of CGS2's three) with the norm of
 each new provisional vector fused into the update (``_dcgs2_step(nrm2=...)``), so the residual test
 of column k needs nothing from column k+1 — no lag, no extra matvec.  Column k's coefficients are
