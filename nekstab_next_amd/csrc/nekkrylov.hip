@@ -103,6 +103,11 @@ static_assert(NKV_FUSE_SMALL_J >= 0 && NKV_FUSE_SMALL_J <= 16,
 #define NKV_D2_MAXB 256  // workgroups of the two-vector multi-dot: one per CU (+1 % over 1024 at
                           // N=1e8 and at the 8-GPU shard; 384 = 1.5 per CU loses 6-10 %)
 #endif
+#ifndef NKV_D2_SMALL_B
+#define NKV_D2_SMALL_B 512  // ... and for small problems (2-row tiles, no field loop): two per CU; the
+                            // kMaxBlocks grid (one tile per block) loses 10-27 % at N=2e6
+                            // (profiles/r03aa_tune_d2_small_grid.log)
+#endif
 #ifndef NKV_D2_FIELDLOOP
 #define NKV_D2_FIELDLOOP 1  // two-vector multi-dot: one block walks all weighted fields of a tile
 #endif
@@ -2171,9 +2176,10 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     // large problems: one block row walks every field of its tiles (weights read once per tile)
     const int nf = (large && NKV_D2_FIELDLOOP) ? L->n_wf : 1;
     const int gy = L->n_wf / nf;
-    // one workgroup per CU for large problems (8 rows/thread keep enough loads in flight); small
-    // problems (2 rows/thread) need the full kMaxBlocks grid to fill the chip
-    int bx = (large ? (NKV_D2_MAXB < kMaxBlocks ? NKV_D2_MAXB : kMaxBlocks) : kMaxBlocks) / gy;
+    // one workgroup per CU for large problems (8 rows/thread keep enough loads in flight); two per
+    // CU for small problems (4 rows/thread), each walking a few tiles
+    const int bmax = large ? NKV_D2_MAXB : NKV_D2_SMALL_B;
+    int bx = (bmax < kMaxBlocks ? bmax : kMaxBlocks) / gy;
     if (bx > tpf) bx = tpf;
     if (bx < 1) bx = 1;
     const int B = bx * gy;

@@ -127,6 +127,16 @@ VARIANTS = {
     # rotation operands, few-column rotation at 9..16 columns) was retired in round 3; its logs stay
     # under profiles/r02*_tune_*.
     "fuse_fw_lds": {"patch": "fuse_fw_lds"},   # fused CGS2 pass: one wave loads f and w per tile
+    "d2_prefetch": {"patch": "d2_prefetch"},   # two-vector multi-dot: next column group loaded during the reduction
+    "d2_prefetch_ps8": {"patch": "d2_prefetch", "NKV_SMALL_TILES": 0},
+    "small_tiles0": {"NKV_SMALL_TILES": 0},
+    "maxb256": {"NKV_MAXB": 256},
+    "maxb512": {"NKV_MAXB": 512},
+    "ps2": {"NKV_PAIRS_SMALL": 2},
+    "d2s_b256": {"NKV_D2_SMALL_B": 256},
+    "d2s_b384": {"NKV_D2_SMALL_B": 384},
+    "d2s_b768": {"NKV_D2_SMALL_B": 768},
+    "d2s_b1024": {"NKV_D2_SMALL_B": 1024},   # the grid before r03aa
     "fmid512": {"NKV_FUSE_G_MID": 512},
     "fmid384": {"NKV_FUSE_G_MID": 384},
     "fmid768": {"NKV_FUSE_G_MID": 768},
