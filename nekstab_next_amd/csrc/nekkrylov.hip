@@ -108,6 +108,10 @@ static_assert(NKV_FUSE_SMALL_J >= 0 && NKV_FUSE_SMALL_J <= 16,
                             // kMaxBlocks grid (one tile per block) loses 10-27 % at N=2e6
                             // (profiles/r03aa_tune_d2_small_grid.log)
 #endif
+#ifndef NKV_DOT_SMALL_B
+#define NKV_DOT_SMALL_B 512  // workgroups of the one-vector multi-dot / dot on small problems: as the
+                            // two-vector one, +6-12 % at N=2e6, j >= 4 (profiles/r03ac_tune_dot_small_grid.log)
+#endif
 #ifndef NKV_D2_FIELDLOOP
 #define NKV_D2_FIELDLOOP 1  // two-vector multi-dot: one block walks all weighted fields of a tile
 #endif
@@ -1850,7 +1854,8 @@ int launch_block_dot_p(const nkv_layout* L, const double* w, const double* Q, in
                        const double* f, double* out, void* ws, unsigned flags, hipStream_t st) {
     constexpr int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
-    int bx = kMaxBlocks / L->n_wf;
+    const int bmax = (P == NKV_PAIRS_SMALL && P != NKV_PAIRS && NKV_DOT_SMALL_B < kMaxBlocks) ? NKV_DOT_SMALL_B : kMaxBlocks;
+    int bx = bmax / L->n_wf;
     if (bx > tpf) bx = tpf;
     if (bx < 1) bx = 1;
     const int B = bx * L->n_wf;

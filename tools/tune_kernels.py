@@ -137,6 +137,9 @@ VARIANTS = {
     "d2s_b384": {"NKV_D2_SMALL_B": 384},
     "d2s_b768": {"NKV_D2_SMALL_B": 768},
     "d2s_b1024": {"NKV_D2_SMALL_B": 1024},   # the grid before r03aa
+    "dots_b1024": {"NKV_DOT_SMALL_B": 1024},   # the grid before r03ac
+    "dots_b256": {"NKV_DOT_SMALL_B": 256},
+    "dots_b768": {"NKV_DOT_SMALL_B": 768},
     "fmid512": {"NKV_FUSE_G_MID": 512},
     "fmid384": {"NKV_FUSE_G_MID": 384},
     "fmid768": {"NKV_FUSE_G_MID": 768},
