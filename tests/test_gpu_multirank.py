@@ -406,6 +406,19 @@ def _run_next(world_rank_pair, out, port, tmpdir):
         info_n = ts_gmres(ctx2, op, rhs, sol_n, GmresConfig(k_dim=12, maxiter=20, tol=1e-14, mode="dcgs2-native"))
         res["gmres_native_equal"] = (info_n.inner_residuals == info.inner_residuals
                                      and bool(torch.equal(sol_n.storage, sol.storage)))
+        # Newton for a periodic orbit: the legacy dispatcher's bordered mode-2.1 map, time in k_dot
+        from nekstab_next_amd.operators import LegacyMatvec
+
+        ctx4 = NekContext(lay2, weights=syn.mass_weights(lay2), comm=comm, max_cols=16, time_in_dot=True)
+        b_fc, b_ic, rhs4, sol4, probe4 = (ctx4.vector() for _ in range(5))
+        for v, sd in ((b_fc, 31), (b_ic, 32), (rhs4, 3), (probe4, 4)):
+            v.fill_hash(sd)
+        b_fc.scal(0.5)
+        b_ic.scal(0.5)
+        rhs4.time = 0.25
+        A4 = LegacyMatvec(2.1, DiagOperator(ctx4, d2), b_fc=b_fc, b_ic=b_ic)
+        info4 = ts_gmres(ctx4, A4, rhs4, sol4, GmresConfig(k_dim=8, maxiter=12, tol=1e-12))
+        res["upo"] = (info4.inner_residuals, info4.outer_residuals, ctx4.dot(sol4, probe4, False), sol4.time)
 
         lay3 = box3d_layout(23).shard(rank, world)
         ctx3 = NekContext(lay3, weights=syn.mass_weights(lay3), comm=comm, max_cols=32)
@@ -436,7 +449,8 @@ def _run_next(world_rank_pair, out, port, tmpdir):
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
     """svds on delayed re-orthogonalisation, GMRES on DCGS2 (Python-driven and the one-call
-    nkv_gmres_dcgs2, identical bit for bit on every rank) and the wave-maker (multi-file mode sets
+    nkv_gmres_dcgs2, identical bit for bit on every rank), a UPO Newton solve through the legacy
+    dispatcher (mode 2.1: period row, time in k_dot) and the wave-maker (multi-file mode sets
     written and read by every rank) on `world` gloo ranks sharing the GPU (4: config 5's split)
     reproduce the one-rank run:
     singular values and C to 1e-12, GMRES histories 1e-8 (the oracle tests' gate) and the solution's projection 1e-12, the
@@ -469,6 +483,12 @@ def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
         np.testing.assert_allclose(o2, o1, rtol=1e-8)
         assert abs(p2 - p1) <= 1e-12 * abs(p1)
         assert got["gmres_native_equal"]   # nkv_gmres_dcgs2 == the Python-driven cycle, bit for bit
+        i1, o1, p1, t1 = one["upo"]
+        i2, o2, p2, t2 = got["upo"]
+        assert len(i1) == len(i2) and len(o1) == len(o2) and len(o1) >= 2
+        np.testing.assert_allclose(i2, i1, rtol=1e-8)
+        np.testing.assert_allclose(o2, o1, rtol=1e-8)
+        assert abs(p2 - p1) <= 1e-10 * abs(p1) and abs(t2 - t1) <= 1e-10 * abs(t1)   # period correction
         ip1, g1 = one["wm"]
         ip2, g2 = got["wm"]
         # the eigenvectors' free phase (dgeev's sign) may differ between world sizes: |<a, d>| and the
