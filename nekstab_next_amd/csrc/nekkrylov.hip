@@ -1090,6 +1090,28 @@ void k_dcgs2_update(const double* __restrict__ Q, int64_t ld, int m,
         return;
     }
     double nrm = 0.0;
+    if (tiles_per_field < (int)gridDim.x && m >= 8) {
+        // small problems: fewer row tiles per field than blocks — one tile per work unit so every
+        // block has work (the weights of a row tile are re-read per field; they stay cache-resident).
+        // +3-8 % at N=2e6 and at the 8-GPU shard for m >= 16; below m = 8 the weight re-reads cost
+        // more than the balance gains (profiles/r03ai_tune_dcgs2_norm_units.log)
+        for (int t = blockIdx.x; t < tiles_total; t += gridDim.x) {
+            const int64_t r0 = (int64_t)t * kTile + 2 * threadIdx.x;
+            dcgs2_tile<kPairs>(Q, ld, m, a, x, rinv, yc, sc, qj, win, f, r0, af);
+            if (t < tiles_w) {
+                const int64_t wr = r0 - (int64_t)(t / tiles_per_field) * sv;
+#pragma unroll
+                for (int k = 0; k < kPairs; ++k) {
+                    const double2 wv = ld2(w + wr + k * 2 * kThreads);
+                    nrm = fma(wv.x * af[k].x, af[k].x, nrm);
+                    nrm = fma(wv.y * af[k].y, af[k].y, nrm);
+                }
+            }
+        }
+        nrm = block_sum(nrm, lds4);
+        if (threadIdx.x == 0) partials[blockIdx.x] = nrm;
+        return;
+    }
     // work unit = one row tile of EVERY weighted field (the norm's weights are read once per unit,
     // not once per field), then the pressure tiles one by one
     const int n_wf = tiles_per_field > 0 ? tiles_w / tiles_per_field : 0;
