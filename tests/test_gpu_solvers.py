@@ -663,3 +663,58 @@ def test_gmres_refuses_a_context_too_small(gpu, mode):
     rhs.fill_hash(3)
     with pytest.raises(ValueError, match="max_cols"):
         ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=12, maxiter=1, mode=mode))
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "dcgs2-native", "cgs2", "mgs2"])
+@pytest.mark.parametrize("ks", [1, 2, 3])
+def test_gmres_tiny_krylov_space_vs_oracle(gpu, mode, ks):
+    """Edge case: ts_gmres with k_dim = 1, 2, 3 (restarted GMRES degenerates towards steepest
+    descent; every cycle opens and closes a one- to three-column factorisation, DCGS2's first step
+    and closing multi-dot back to back).  Histories 1e-8 and the solution 1e-10 against the oracle."""
+    lay = cylinder_layout(60)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=8)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    op = ShiftedOperator(DiagOperator(ctx, d), -1.0)
+    rhs = ctx.vector()
+    rhs.fill_hash(3)
+    sol = ctx.vector()
+    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=ks, maxiter=15, tol=1e-12, mode=mode))
+    J = syn.to_reference_order(lay, d) - 1.0
+
+    def mv(x, y):
+        y[:] = J * x
+        y[-1] = 0.0
+
+    rref = syn.to_reference_order(lay, syn.hash_vector(lay, 3))
+    sref, hist = orc.ts_gmres(L, w, mv, rref, maxiter=15, ksize=ks, tol=1e-12)
+    assert len(info.outer_residuals) == len(hist["outer"]) == 15
+    assert len(info.inner_residuals) == len(hist["inner"])
+    np.testing.assert_allclose(info.inner_residuals, hist["inner"], rtol=1e-8)
+    np.testing.assert_allclose(info.outer_residuals, hist["outer"], rtol=1e-8)
+    got = syn.to_reference_order(lay, sol.to_packed())
+    nw = L.nwf * L.nv
+    diff = got[:nw] - sref[:nw]
+    assert np.sqrt(np.sum(np.tile(w, L.nwf) * diff * diff)) < 1e-10 * max(1.0, np.sqrt(np.sum(np.tile(w, L.nwf) * sref[:nw] ** 2)))
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "mgs2"])
+@pytest.mark.parametrize("k_dim,tgt", [(8, 1), (10, 2)])
+def test_krylov_schur_small_k_dim_vs_oracle(gpu, mode, k_dim, tgt):
+    """Edge case: Krylov–Schur with a Krylov space of 8 or 10 vectors and 1 or 2 wanted eigenvalues
+    (the smallest spaces in which the nev + 4 kept Schur vectors leave room to grow):
+    many restarts, each keeping only a few Schur vectors.  Restart trajectory identical to the
+    oracle's, Ritz values 1e-10."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16)
+    L = olayout(lay)
+    d, exact = syn.diag_spectrum(lay)
+    seed, q1 = _seed(ctx, lay, L, w)
+    cfg = KrylovSchurConfig(k_dim=k_dim, schur_tgt=tgt, mode=mode, max_restarts=200)
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)
+    ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, k_dim, tgt,
+                           max_restarts=200)
+    assert res.schur_cnt >= 1
+    _compare_ks(res, ref, cfg)
