@@ -718,3 +718,34 @@ def test_krylov_schur_small_k_dim_vs_oracle(gpu, mode, k_dim, tgt):
                            max_restarts=200)
     assert res.schur_cnt >= 1
     _compare_ks(res, ref, cfg)
+
+
+@pytest.mark.parametrize("mode", ["dcgs2", "dcgs2-native", "cgs2"])
+def test_gmres_invariant_krylov_space(gpu, mode):
+    """Edge case: an operator with two distinct eigenvalues, so the Krylov space is invariant after
+    two columns and GMRES's residual drops to rounding level there ("happy breakdown").  The
+    reference exits on beta**2 < tol before normalising a zero vector; so must every mode — no NaN
+    from the closing re-orthogonalisation of the (rounding-noise) next vector, the exact solution to
+    1e-12, and the same history as the oracle."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=20)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16)
+    L = olayout(lay)
+    d = np.zeros(lay.ld)
+    for f in range(lay.n_wf):
+        d[f * lay.sv: f * lay.sv + lay.n_v] = 2.0 if f == 0 else 0.5
+    d[lay.n_wf * lay.sv: lay.n_wf * lay.sv + lay.n_p] = 2.0
+    op = DiagOperator(ctx, d)
+    rhs = ctx.vector()
+    rhs.fill_hash(3)
+    sol = ctx.vector()
+    info = ts_gmres(ctx, op, rhs, sol, GmresConfig(k_dim=8, maxiter=3, tol=1e-20, mode=mode))
+    dref = syn.to_reference_order(lay, d)
+    rref = syn.to_reference_order(lay, syn.hash_vector(lay, 3))
+    sref, hist = orc.ts_gmres(L, w, oracle_diag_matvec(L, dref), rref, maxiter=3, ksize=8, tol=1e-20)
+    got = syn.to_reference_order(lay, sol.to_packed())
+    n = L.n
+    exact = rref[:n] / dref[:n]
+    assert np.max(np.abs(got[:n] - exact)) <= 1e-12 * np.max(np.abs(exact))
+    assert np.max(np.abs(sref[:n] - exact)) <= 1e-12 * np.max(np.abs(exact))
+    assert info.outer_residuals[0] < 1e-20 and hist["outer"][0] < 1e-20
