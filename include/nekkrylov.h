@@ -371,7 +371,7 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
  * overwritten with its triangularised form), cs/sn: the k rotations so far (the new one appended at
  * index k), g: k+2 doubles, g[0] = beta before the first column.  The reference solves the whole
  * system with dgels at every column for this number (:255-258); y itself still comes from dgels on
- * the final system. */
+ * the final system.  k < 0 or a NULL array: returns NaN (message in nkv_last_error). */
 double nkv_givens_column(int k, double* h, double* cs, double* sn, double* g);
 
 /* ---- shard-independent synthetic data ----------------------------------------------------

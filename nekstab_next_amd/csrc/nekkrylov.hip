@@ -3008,6 +3008,10 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
 // updated; g[0] = beta on the first call).  Returns |g[k+1]| = ||beta e_1 - H y|| of the (k+2) x (k+1)
 // least-squares problem; h is overwritten with the triangularised column.
 double nkv_givens_column(int k, double* h, double* cs, double* sn, double* g) {
+    if (k < 0 || !h || !cs || !sn || !g) {   // no status channel: a NaN residual never passes a test
+        fail(NKV_EINVAL, "givens: k=%d or a NULL array", k);
+        return std::nan("");
+    }
     for (int i = 0; i < k; ++i) {
         const double t = cs[i] * h[i] + sn[i] * h[i + 1];
         h[i + 1] = -sn[i] * h[i] + cs[i] * h[i + 1];

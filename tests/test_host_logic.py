@@ -181,3 +181,19 @@ def test_givens_residual_equals_least_squares_residual():
     H = np.array([[2.0, 1.0], [0.0, 3.0], [0.0, 0.0]])   # H(2,1) = 0: exact after one column
     g = GivensResidual(1.0, 2)
     assert g.add_column(H[:2, 0]) == 0.0
+
+
+def test_givens_column_rejects_bad_input():
+    """nkv_givens_column has no status channel: bad input returns NaN (so a residual test on it never
+    passes) and leaves a message in nkv_last_error."""
+    import ctypes
+
+    from nekstab_next_amd import _lib
+
+    lib = _lib.load()
+    a = np.zeros(4)
+    p = a.ctypes.data
+    assert np.isnan(lib.nkv_givens_column(-1, p, p, p, p))
+    assert np.isnan(lib.nkv_givens_column(0, None, p, p, p))
+    assert "givens" in _lib.last_error()
+    assert not np.isnan(lib.nkv_givens_column(0, p, p, p, p))
