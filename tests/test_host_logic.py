@@ -186,8 +186,6 @@ def test_givens_residual_equals_least_squares_residual():
 def test_givens_column_rejects_bad_input():
     """nkv_givens_column has no status channel: bad input returns NaN (so a residual test on it never
     passes) and leaves a message in nkv_last_error."""
-    import ctypes
-
     from nekstab_next_amd import _lib
 
     lib = _lib.load()
