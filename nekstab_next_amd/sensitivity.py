@@ -12,6 +12,10 @@ the adjoint mode (all fields incl. pressure and scalars; ``time`` untouched) so 
 kernel, ``nkv_wavemaker``) and write it as the temperature field of ``wm_<session>0.f00001``
 (:73-74).  It needs no derivatives.  The base-flow sensitivity (``bf_sensitivity``, :81-269) does
 — Nek5000's ``gradm1``/``dsavg`` on the spectral-element mesh — and stays out of scope.
+
+``ts_steady_force_sensitivity`` (:273-346): GMRES on the time-stepper form of the steady-force
+sensitivity problem, ``ts_gmres`` over the legacy dispatcher's mode-4 map; the forced Nek5000 run
+that recasts the right-hand side is the caller's.
 """
 from __future__ import annotations
 
@@ -119,3 +123,48 @@ def wave_maker(ctx: NekContext, directory: str, session: str = "nek", d_num: int
     fld.write_fld(path, f)
     return dict(wavemaker=wm, inner_product=ip, path=path, vectors=(dRe, dIm, aRe, aIm))
 
+
+
+def ts_steady_force_sensitivity(ctx: NekContext, op, directory: str, session: str = "nek", part: str = "r",
+                                recast=None, k_dim: int = 100, tol: float = 1e-9, outdir: str | None = None,
+                                mode: str | None = None) -> dict:
+    """``ts_steady_force_sensitivity`` (sensitivity.f90:273-346, Marquet, Sipp & Jacquin 2008): the
+    sensitivity of the flow to a steady force, by GMRES on the time-stepper form of the adjoint
+    problem.  ``part`` "r" (uparam(1) = 4.41) reads the velocity of ``sr_<session>0.f00001``, "i"
+    (4.42) that of ``si_<session>0.f00001`` (``opcopy``, :317-325; the other fields start at zero);
+    ``recast(rhs)`` is ``initialize_rhs_ts_steady_force_sensitivity`` (:350-391), a forced adjoint
+    Nek5000 integration that maps the forcing to the time-stepper right-hand side in place — the
+    caller's (identity when omitted).  Then k_normalize (alpha), ``ts_gmres(rhs, sol, 10, k_dim)``
+    on ``ts_force_sensitivity_map`` (q - exp(tL^T) q: :class:`~.operators.LegacyMatvec` mode 4.x
+    over ``op.rmatvec``), sol *= alpha, and ``outpost`` of sol as ``fsr``/``fsi`` (Nek5000 names the
+    file ``fsr<session>0.f00001``).  Returns the solution, alpha, the GMRES record and the file."""
+    from . import fld
+    from .config import GmresConfig
+    from .gmres import ts_gmres
+    from .operators import LegacyMatvec
+    from .vector import k_cmult, k_normalize
+
+    if part not in ("r", "i"):
+        raise ValueError("part must be 'r' (uparam(1) = 4.41) or 'i' (4.42)")
+    lay = ctx.layout
+    files = fld.read_fld_set(directory, f"s{part}_", session, 1)
+    if not files:
+        raise FileNotFoundError(f"{fld.fld_name(f's{part}_', session, 0, 1)} not found in {directory}")
+    full = fld.vector_from_fld(lay, files)
+    host = np.zeros(lay.ld)
+    for c in range(lay.ldim):   # opcopy: the velocity components only
+        host[c * lay.sv: c * lay.sv + lay.n_v] = full[c * lay.sv: c * lay.sv + lay.n_v]
+    rhs = ctx.vector().from_packed(host)
+    if recast is not None:
+        recast(rhs)
+    alpha = k_normalize(rhs)
+    sol = ctx.vector()
+    cfg = GmresConfig(k_dim=k_dim, maxiter=10, tol=tol, **({"mode": mode} if mode else {}))
+    info = ts_gmres(ctx, LegacyMatvec(4.41 if part == "r" else 4.42, op), rhs, sol, cfg)
+    k_cmult(sol, alpha)
+    ctx.check_nan()
+    out = outdir or directory
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, fld.fld_name(f"fs{part}", session, lay.rank, 1))
+    fld.write_fld(path, fld.fld_from_vector(lay, sol.to_packed(), time=files[0].time, istep=1))
+    return dict(solution=sol, alpha=alpha, info=info, path=path)

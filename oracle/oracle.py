@@ -9,7 +9,8 @@ What it restates (each function cites the reference line it follows):
   ordering rules ``quicksort2`` / ``select_eigenvalues`` / ``sort_eigendecomp``: plain C in
   ``nekstab_oracle.c`` (reference operation order, no FP contraction);
 * the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
-  ``ts_gmres``, ``biorthogonalize``, ``wave_maker``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
+  ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, the legacy ``matvec`` dispatcher,
+  ``ts_steady_force_sensitivity``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
   dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
 
 Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
@@ -463,6 +464,21 @@ def legacy_matvec(L: OLayout, w, mode, fwd, adj, f, q, fd=None, b_fc=None, b_ic=
             f[-1] = 0.0
         return "n"
     raise ValueError(f"uparam(1)={mode} selects no map")
+
+
+def ts_steady_force_sensitivity(L: OLayout, w, adj, rhs, k_dim, tol, part="r", recast=None):
+    """sensitivity.f90:273-346 after the load: ``rhs`` holds the forcing's velocity (other fields 0);
+    recast (the forced run, :331), k_normalize (:334), ts_gmres(rhs, sol, 10, k_dim) on the mode-4
+    map of ``matvec`` (:337, matvec.f90:134-136, 499-516), sol *= alpha (:340).  Returns (sol, hist,
+    alpha)."""
+    rhs = np.array(rhs, dtype=np.float64)
+    if recast is not None:
+        recast(rhs)
+    alpha = k_normalize(L, w, rhs)
+    mode = 4.41 if part == "r" else 4.42
+    sol, hist = ts_gmres(L, w, lambda x, y: legacy_matvec(L, w, mode, None, adj, y, x), rhs, 10, k_dim, tol)
+    lib().orc_k_cmult(ctypes.byref(L.c), sol, alpha)
+    return sol, hist, alpha
 
 
 def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):

@@ -17,6 +17,7 @@ import torch
 
 import nekio
 import oracle as orc
+from helpers import olayout, oracle_rank2_matvec
 from nekstab_next_amd import fld
 from nekstab_next_amd import synthetic as syn
 from nekstab_next_amd.config import KrylovSchurConfig
@@ -208,3 +209,48 @@ def test_wave_maker_config5_full_size(gpu, tmp_path):
     assert f.rdcode == "T" and np.array_equal(np.asarray(f.fields["t"]).ravel(), res["wavemaker"])
     tok, ids, fields = nekio.read_std(res["path"])
     assert tok[11] == "T" and ids.size == 22088 and np.array_equal(fields["t"].ravel(), res["wavemaker"])
+
+
+@pytest.mark.parametrize("part", ["r", "i"])
+def test_steady_force_sensitivity_vs_oracle(gpu, tmp_path, part):
+    """ts_steady_force_sensitivity (sensitivity.f90:273-346): the forcing's velocity read from
+    ``s<part>_<session>0.f00001`` (written by the oracle's own #std writer, pressure and scalars
+    present and ignored), GMRES on the mode-4 map q - A^T q of a non-normal operator, sol * alpha
+    written as ``fs<part><session>0.f00001``.  GMRES histories 1e-8 and the solution 1e-10 against the
+    oracle's restatement; the written file read back by the oracle's reader."""
+    from nekstab_next_amd.sensitivity import ts_steady_force_sensitivity
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=120, n_scalars=1)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=24)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    d = 0.5 * d
+    vs = []
+    for s5 in (21, 22, 23, 24):
+        v = ctx.vector()
+        v.fill_hash(s5)
+        v.scal(0.05)
+        vs.append(v)
+    A = RankTwoPerturbed(DiagOperator(ctx, d), *vs, sigma=2.0)
+    adj = oracle_rank2_matvec(lay, d, *(0.05 * syn.hash_vector(lay, s5) for s5 in (21, 22, 23, 24)), 2.0, w,
+                              transpose=True)
+    g = nekio.Geom(lay.ldim, lay.lx1, lay.lx2, lay.nelgv, 0, lay.nelgv, lay.n_scalars)
+    forcing = syn.to_reference_order(lay, syn.hash_vector(lay, 5))
+    nekio.write_std(str(tmp_path / f"s{part}_cyl0.f00001"), g, forcing)
+    r = ts_steady_force_sensitivity(ctx, A, str(tmp_path), session="cyl", part=part, k_dim=20, tol=1e-14)
+    rhs = nekio.read_std_vector([str(tmp_path / f"s{part}_cyl0.f00001")], g)
+    nvel = lay.ldim * lay.n_v
+    rhs[nvel:] = 0.0                                  # opcopy: velocity only
+    sref, hist, alpha = orc.ts_steady_force_sensitivity(L, w, adj, rhs, 20, 1e-14, part=part)
+    assert abs(r["alpha"] - alpha) <= 1e-12 * alpha
+    assert len(r["info"].outer_residuals) == len(hist["outer"]) >= 1
+    assert len(r["info"].inner_residuals) == len(hist["inner"])
+    np.testing.assert_allclose(r["info"].inner_residuals, hist["inner"], rtol=1e-8)
+    np.testing.assert_allclose(r["info"].outer_residuals, hist["outer"], rtol=1e-8)
+    got = syn.to_reference_order(lay, r["solution"].to_packed())
+    n = L.n
+    assert np.max(np.abs(got[:n] - sref[:n])) <= 1e-10 * np.max(np.abs(sref[:n]))
+    back = nekio.read_std_vector([r["path"]], g)
+    assert np.max(np.abs(back[:nvel] - got[:nvel])) == 0.0   # 64-bit file, velocity bit for bit
+    assert r["path"].endswith(f"fs{part}cyl0.f00001")

@@ -194,3 +194,21 @@ def test_legacy_matvec_closed_forms():
         assert abs(f[-1] - time) <= 1e-12 * max(1.0, abs(time))
     with pytest.raises(ValueError):
         orc.legacy_matvec(L, w, 3.4, mv, mv, np.zeros(L.len), q)
+
+
+def test_steady_force_sensitivity_closed_form():
+    """oracle.ts_steady_force_sensitivity (sensitivity.f90:273-346) with a diagonal adjoint map D and
+    no recast: GMRES on q - D q, so the solution is the forcing / (1 - d) on the velocity (other
+    fields 0), to 1e-10 after its 10 restarts."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=40)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    d = 0.5 * syn.to_reference_order(lay, syn.diag_spectrum(lay)[0])
+    rhs = syn.to_reference_order(lay, syn.hash_vector(lay, 5))
+    nvel = lay.ldim * lay.n_v
+    rhs[nvel:] = 0.0
+    sol, hist, alpha = orc.ts_steady_force_sensitivity(L, w, oracle_diag_matvec(L, d), rhs, 20, 1e-24)
+    exact = np.zeros_like(rhs)
+    exact[:nvel] = rhs[:nvel] / (1.0 - d[:nvel])
+    assert np.max(np.abs(sol[:-1] - exact[:-1])) <= 1e-10 * np.max(np.abs(exact))
+    assert hist["outer"][-1] < 1e-20
