@@ -1,0 +1,75 @@
+"""Newton–Krylov for fixed points of a time-stepper (nekStab's ``newton_krylov``, the caller of
+config 4's GMRES).
+
+Reference: ``core/newton_krylov.f90:1-166``.  Per Newton iteration i (at most 100, :44):
+
+    f = F(q)                          nonlinear_forward_map (:97): a Nek5000 run, the caller's map
+    residual = ||f||**2               k_norm (:102), written to residu_newton.dat (:109)
+    exit if residual < tol            (:112; tol = max(param(21), param(22)), :37-41)
+    ts_gmres(f, dq, 100, k_dim)       on the linearised map at q (:120): the legacy dispatcher's
+                                      newton_linearized_map, uparam(1) = 2.x (matvec.f90:520-571)
+    q = q - dq                        k_sub2 (:125), time included
+
+and on convergence q is written as the base flow ``BF_<session>0.f00001`` (:155-164).  The
+caller supplies ``nonlinear(q, f)`` (f <- F(q)) and ``linearized(q)`` (a LinearOperator: the
+forward map of the linearisation about q; for uparam(1) = 2.1 wrap the period row with
+:class:`~.operators.LegacyMatvec` yourself and pass ``mode=2.1``).  Out of scope, as in SURVEY §2:
+the dynamic tolerance schedule (``ifdyntol``, ``spec_tole``, :93, :114-117, :383-435), the orbit
+storage for UPOs (:82-91) and the Nek5000 output of intermediate iterates (``nwt``, ``ic_``)."""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+from .config import GmresConfig
+from .gmres import ts_gmres
+from .operators import LegacyMatvec
+from .vector import NekContext, NekVector, k_dot, k_sub2
+
+
+@dataclass
+class NewtonResult:
+    converged: bool
+    iterations: int
+    residuals: list = field(default_factory=list)       # ||F(q)||^2 per iteration (residu_newton.dat)
+    gmres: list = field(default_factory=list)           # the GmresInfo of every linear solve
+    path: str | None = None
+
+
+def newton_krylov(ctx: NekContext, nonlinear, linearized, q: NekVector, tol: float = 1e-9, maxiter: int = 100,
+                  gmres: GmresConfig | None = None, mode: float = 2.0, fd: bool = False, outdir: str | None = None,
+                  session: str = "nek") -> NewtonResult:
+    """q is updated in place (the current estimate, as nekStab's ``q``).  ``gmres`` defaults to the
+    reference's inner solve: maxiter 100 (:44), ``k_dim`` from the configuration, the same
+    tolerance; ``fd`` selects the finite-difference exits (``iffindiff``).  ``mode`` is uparam(1)
+    for the linearised map (2.0 / 2.1 / 2.2)."""
+    gcfg = gmres or GmresConfig(maxiter=100, tol=tol, findiff=fd)
+    res = NewtonResult(False, 0)
+    f = ctx.vector()
+    dq = ctx.vector()
+    lines = []
+    for i in range(1, maxiter + 1):
+        nonlinear(q, f)
+        residual = k_dot(f, f)
+        res.residuals.append(residual)
+        res.iterations = i
+        lines.append(f"{i:6d}{residual:15.7E}\n")
+        if residual < tol:
+            res.converged = True
+            break
+        op = linearized(q)
+        if not isinstance(op, LegacyMatvec):
+            op = LegacyMatvec(mode, op)
+        res.gmres.append(ts_gmres(ctx, op, f, dq, gcfg))
+        k_sub2(q, dq)
+    if outdir is not None and ctx.comm.rank == 0:
+        os.makedirs(outdir, exist_ok=True)
+        with open(os.path.join(outdir, "residu_newton.dat"), "w") as fh:
+            fh.writelines(lines)
+    if outdir is not None and res.converged:
+        from . import fld
+
+        lay = ctx.layout
+        res.path = os.path.join(outdir, fld.fld_name("BF_", session, lay.rank, 1))
+        fld.write_fld(res.path, fld.fld_from_vector(lay, q.to_packed(), time=q.time, istep=res.iterations))
+    return res

@@ -10,7 +10,7 @@ What it restates (each function cites the reference line it follows):
   ``nekstab_oracle.c`` (reference operation order, no FP contraction);
 * the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
   ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, the legacy ``matvec`` dispatcher,
-  ``ts_steady_force_sensitivity``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
+  ``ts_steady_force_sensitivity``, ``newton_krylov``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
   dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
 
 Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
@@ -479,6 +479,31 @@ def ts_steady_force_sensitivity(L: OLayout, w, adj, rhs, k_dim, tol, part="r", r
     sol, hist = ts_gmres(L, w, lambda x, y: legacy_matvec(L, w, mode, None, adj, y, x), rhs, 10, k_dim, tol)
     lib().orc_k_cmult(ctypes.byref(L.c), sol, alpha)
     return sol, hist, alpha
+
+
+def newton_krylov(L: OLayout, w, nonlinear, linearized, q, tol, maxiter, ksize, gmres_maxiter=100, mode=2.0,
+                  gmres_tol=None):
+    """newton_krylov.f90:1-166 without the dynamic tolerance: f = F(q) (:97), residual = k_norm**2
+    (:102), exit below tol (:112), ts_gmres(f, dq, 100, k_dim) on newton_linearized_map about q
+    (:120, matvec.f90:520-571 via legacy_matvec), q = q - dq (k_sub2, :125).  ``linearized(q)``
+    returns the forward map m(x, y) of the linearisation about q.  Returns (q, residuals, gmres
+    histories)."""
+    q = np.array(q, dtype=np.float64)
+    c = ctypes.byref(L.c)
+    residuals, hists = [], []
+    for _i in range(maxiter):
+        f = L.zeros()
+        nonlinear(q, f)
+        r = k_dot(L, w, f, f)
+        residuals.append(r)
+        if r < tol:
+            break
+        fwd = linearized(q)
+        dq, hist = ts_gmres(L, w, lambda x, y: legacy_matvec(L, w, mode, fwd, None, y, x), f, gmres_maxiter, ksize,
+                            tol if gmres_tol is None else gmres_tol)
+        hists.append(hist)
+        lib().orc_k_sub2(c, q, dq)
+    return q, residuals, hists
 
 
 def biorthogonalize(L: OLayout, w, dRe, dIm, aRe, aIm):

@@ -212,3 +212,36 @@ def test_steady_force_sensitivity_closed_form():
     exact[:nvel] = rhs[:nvel] / (1.0 - d[:nvel])
     assert np.max(np.abs(sol[:-1] - exact[:-1])) <= 1e-10 * np.max(np.abs(exact))
     assert hist["outer"][-1] < 1e-20
+
+
+def test_newton_krylov_closed_form():
+    """oracle.newton_krylov (newton_krylov.f90:1-166) on the pointwise quadratic fixed point
+    q = d q + c + eps q^2: from q = 0 Newton reaches, at every point, the root of
+    eps q^2 + (d - 1) q + c = 0 nearest 0, quadratically, to 1e-12 in the W-norm (GMRES minimises
+    the k_dot norm, which leaves pressure out)."""
+    import ctypes
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=30)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    eps = 0.3
+    d = 0.5 * syn.to_reference_order(lay, syn.diag_spectrum(lay)[0])
+    c = 0.05 * syn.to_reference_order(lay, syn.hash_vector(lay, 8))
+    live = np.ones(L.len)
+    live[-1] = 0.0
+
+    def onl(x, y):
+        y[:] = (d * x + c + eps * x * x - x) * live
+
+    def olin(x0):
+        g = (d + 2.0 * eps * x0) * live
+        return lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), g, x, y, 0.0)
+
+    q, r, _ = orc.newton_krylov(L, w, onl, olin, L.zeros(), 1e-24, 10, 20)
+    b = d - 1.0
+    root = 2.0 * c / (-b + np.sqrt(b * b - 4.0 * eps * c))   # the root through q = 0 as c -> 0 (stable form)
+    # GMRES minimises in the W-norm of k_dot (weighted fields only): gate the weighted velocity error
+    nvel = lay.ldim * lay.n_v
+    err = q[:nvel] - root[:nvel]
+    assert np.sqrt(np.sum(np.tile(w, lay.ldim) * err * err)) <= 1e-12
+    assert r[-1] < 1e-24 and r[2] < 1e-5 * r[1]
