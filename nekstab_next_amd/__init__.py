@@ -14,8 +14,8 @@ def __getattr__(name):
     # build host without a GPU; they raise loudly on first use if the HIP library or the GPU is absent.
     import importlib
 
-    for mod in ("vector", "operators", "arnoldi", "krylov_schur", "gmres", "sensitivity", "lapack", "comm",
-                "synthetic", "_lib"):
+    for mod in ("vector", "operators", "arnoldi", "krylov_schur", "gmres", "newton", "sensitivity", "lapack",
+                "comm", "synthetic", "lightkrylov", "drivers", "checkpoint", "fld", "boostconv", "_lib"):
         if name == mod:
             return importlib.import_module(f".{mod}", __name__)
     raise AttributeError(name)
