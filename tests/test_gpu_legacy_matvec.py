@@ -112,3 +112,45 @@ def test_upo_newton_gmres_vs_oracle(gpu, mode):
     scale = max(1.0, np.sqrt(orc.k_dot(L, w, sref, sref)))   # D - I is nearly singular: ||sol|| >> 1
     assert np.sqrt(orc.k_dot(L, w, diff, diff)) < 1e-10 * scale
     assert abs(sref[-1]) > 1e-6                 # the period correction is part of the solution
+
+
+@pytest.mark.gpu
+def test_transient_growth_map_krylov_schur_vs_oracle_and_svds(gpu):
+    """uparam(1) = 3.3: the in-tree Krylov–Schur on transient_growth_map (adjoint∘forward,
+    matvec.f90:478-495; evop 'p') against the oracle's Krylov–Schur on its restatement of the same
+    map (trajectory and Ritz values 1e-10), and against the LightKrylov-style svds of the forward map
+    (transient_growth_analysis, linear_stab.f90:82-119): the leading eigenvalues are sigma^2 (1e-10)."""
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.krylov_schur import krylov_schur, prepare_seed
+    from nekstab_next_amd.lightkrylov import svds
+    from nekstab_next_amd.operators import RankTwoPerturbed
+    from helpers import match_ritz, oracle_rank2_matvec, ritz_compare_set
+
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=200)
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=40)
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    hv = [0.05 * syn.hash_vector(lay, s5) for s5 in (21, 22, 23, 24)]
+    vs = [ctx.vector().from_packed(v) for v in hv]
+    A = RankTwoPerturbed(DiagOperator(ctx, d), *vs, sigma=2.0)
+    P = LegacyMatvec(3.3, A)
+    assert P.evop == "p"
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    cfg = KrylovSchurConfig(k_dim=24, schur_tgt=3)
+    res = krylov_schur(ctx, P, seed, cfg)
+    fwd = oracle_rank2_matvec(lay, d, *hv, 2.0, w)
+    adj = oracle_rank2_matvec(lay, d, *hv, 2.0, w, transpose=True)
+    q1 = orc.prepare_seed(L, w, syn.to_reference_order(lay, syn.hash_vector(lay, 11)))
+    ref = orc.krylov_schur(L, w, lambda x, y: orc.legacy_matvec(L, w, 3.3, fwd, adj, y, x), q1, 24, 3)
+    assert res.schur_cnt == ref["schur_cnt"] and res.mstart_history == ref["mstart"]
+    sel = ritz_compare_set(ref["vals"], ref["residual"], cfg.eigen_tol)
+    got = match_ritz(ref["vals"][sel], res.vals)
+    assert np.max(np.abs(got - ref["vals"][sel]) / np.abs(ref["vals"][sel])) <= 1e-10
+    # the same gains from the bidiagonalisation of A
+    U, V = ctx.basis(25), ctx.basis(25)
+    prepare_seed(seed, V[0])
+    sv = svds(ctx, A, U, V, nev=3, tolerance=1e-10)
+    conv = np.sort(res.vals[res.residual < 1e-8].real)[::-1][:3]
+    np.testing.assert_allclose(conv, np.sort(sv.sigma ** 2)[::-1][:3], rtol=1e-10)
