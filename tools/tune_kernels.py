@@ -149,6 +149,13 @@ VARIANTS = {
     "d2u4": {"NKV_D2_U": 4},
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
     "d2red": {"NKV_D2_RED": 1},
+    # two-vector multi-dot split into column groups at j >= NKV_D2_CG_J (round 3): fewer pages per CU
+    "d2cs2": {"patch": "d2_colsplit"},                                  # 2 groups, 256 workgroups in all
+    "d2cs2_b512": {"patch": "d2_colsplit", "NKV_D2_CG_B": 512},          # 2 groups x 256 (same tiles per block)
+    "d2cs4_b512": {"patch": "d2_colsplit", "NKV_D2_CG": 4, "NKV_D2_CG_B": 512},
+    "d2cs4_b1024": {"patch": "d2_colsplit", "NKV_D2_CG": 4, "NKV_D2_CG_B": 1024},
+    "d2cs2_j32": {"patch": "d2_colsplit", "NKV_D2_CG_J": 32},
+    "d2cs2_b512_j32": {"patch": "d2_colsplit", "NKV_D2_CG_B": 512, "NKV_D2_CG_J": 32},
 }
 
 
