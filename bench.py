@@ -80,7 +80,8 @@ def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
     """HBM bytes the executed algorithm moves per factorisation (global sizes), per kernel:
     block_dot 8(jN_w + N_w + n_v); fused update_dot 8(jN + 2N + n_v); update+norm 8(jN + 2N + n_v);
     finish 8(2N); diag matvec 8(3N); DCGS2 dual update 8((j-1)N + 4N), over a lazy basis (one
-    output vector) 8(jN + 2N); mgs2 (the reference's order) one dot 8(2N_w + n_v), then per column
+    output vector) 8(jN + 2N); mgs2-icwy: a two-vector dot 8((j-1)N_w + 2N_w + n_v) then the cgs2 update_dot and
+    update+norm; mgs2 (the reference's order) one dot 8(2N_w + n_v), then per column
     and pass one fused axpy + next dot (nkv_axpy_dot) 8(3N + N_w + n_v), the last one's dot the norm.  A "-native" mode moves the bytes of its twin."""
     mode = mode.replace("-native", "")
     tot = 0.0
@@ -91,6 +92,8 @@ def executed_bytes(N, N_w, n_v, m, mode, lazy=False):
             tot += 8.0 * (2 * N_w + n_v) + 2 * j * 8.0 * (3 * N + N_w + n_v) - 8.0 * N_w
         elif mode == "cgs2":
             tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
+        elif mode == "mgs2-icwy":   # two-vector dot (Gram row + pass-1 dots), fused update+dot, update+norm
+            tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v) + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
         elif mode == "cgs2-unfused":
             tot += 2 * dot + upd + (upd + 8.0 * n_v)
         elif mode == "dcgs2":   # two-vector dot over j-1 streamed columns (+ u, A u); dual update over j-1
@@ -300,7 +303,7 @@ def parse_args(argv=None):
     ap.add_argument("--m", type=int, default=128)
     ap.add_argument("--mode", default="dcgs2",
                     help="dcgs2 (default) | cgs2 | cgs2-unfused | mgs2 (reference order) | dcgs2-native | "
-                         "cgs2-native | mgs2-native (the one-call C drivers)")
+                         "cgs2-native | mgs2-native (the one-call C drivers) | mgs2-icwy (MGS in inverse compact WY form)")
     ap.add_argument("--lazy-basis", action="store_true",
                     help="dcgs2 over a lazy basis Q = S T (one vector write less per step)")
     ap.add_argument("--cpu-E", type=int, default=11044, help="CPU baseline sample (11,044 -> N=2.5e7)")

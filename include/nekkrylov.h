@@ -75,7 +75,7 @@ extern "C" {
 #define NKV_ACCUMULATE 0x2u /* block_update: f <- f - Q h   (default)                             */
 #define NKV_OVERWRITE 0x4u  /* block_update: f <- + Q h     (k_matmul, krylov_subspace.f90:163)    */
 #define NKV_NORM2 0x8u      /* block_update: also write the local ||f||_W^2 partial               */
-#define NKV_TIME_DOT 0x10u  /* block_update_dot: include the time product in the dot partial      */
+#define NKV_TIME_DOT 0x10u  /* block_update_dot / block_update+NORM2: time product in the dot/norm */
 #define NKV_X_IS_LAST 0x20u /* block_dot2: x is column j-1 of Q (its two dots come from registers)  */
 #define NKV_MGS2 0x40u      /* update_hessenberg / arnoldi_factorization: the reference's MGS2 order */
 #define NKV_CHECK_BREAKDOWN 0x80u /* one-call factorisations: check the new H columns on return      */
@@ -133,7 +133,8 @@ int nkv_dot(const nkv_layout* L, const double* w, const double* a, const double*
  * block_dot:    h_dev[0:j] = Q[:,0:j]^T W f  (LOCAL partials, deterministic 2-stage reduction)
  * block_update: f <- f - Q[:,0:j] h           (NKV_ACCUMULATE, default)
  *               f <- Q[:,0:j] h               (NKV_OVERWRITE: k_matmul / mode reconstruction)
- *               with NKV_NORM2 also nrm2_dev[0] = ||f_new||_W^2 local partial (+time term)
+ *               with NKV_NORM2 also nrm2_dev[0] = ||f_new||_W^2 local partial (+ f.time^2 with
+ *               NKV_TIME_DOT on rank0; NKV_TIME alone updates the slot, not the norm)
  * arnoldi_finish: q_out = f/beta, beta = sqrt(nrm2_dev[0]); H column k written on the device:
  *               hcol[i] = h1[i] + h2[i] (i<j; h2 may be NULL), hcol[j] = beta (H(k+1,k), :183-186) */
 int nkv_block_dot(const nkv_layout* L, const double* w, const double* Q, int j, const double* f,
@@ -198,6 +199,26 @@ int nkv_dcgs2_coef(int m, const double* hq_dev, const double* hw_dev, const doub
 int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int m, const double* coef_dev,
                      double* qj, const double* win, double* fout, double* nrm2_dev, void* ws, unsigned flags,
                      void* stream);
+
+/* ---- MGS2 in inverse compact WY form (mode "mgs2-icwy"; Swirydowicz et al. 2020) -----------
+ * One modified Gram–Schmidt pass of update_hessenberg_matrix (krylov_decomposition.f90:155-168,
+ * repeated at :171-180) over q_0..q_{j-1}: alpha_i = <f_i, q_i>_W with f_i = f - sum_{k<i} alpha_k q_k.
+ * In exact arithmetic alpha_i = b_i - sum_{k<i} G(i,k) alpha_k with b = Q^T W f (classical dots) and
+ * G(i,k) = <q_k, q_i>_W, whether or not the basis is orthonormal (it is not after the reference's
+ * unnormalised noise/load seed, eigensolvers.f90:192-223, or a restart with time in k_dot), so
+ * alpha = (I + L)^{-1} b, L the strictly lower part of G: the pass becomes one multi-dot, this
+ * O(j^2) solve (one workgroup, no host sync) and one block update — three reads of Q per step for
+ * both passes instead of the reference order's per-column stream of f.
+ * G: row-major, row i at G + i*ldg (ldg >= j); columns k < i are read.  grow (may be NULL): the
+ * row G(j-1, 0:j-1) of the newest column, stored into G first (nkv_block_dot2's first j-1 entries
+ * with x = q_{j-1}).  x may alias b.  Step j of the factorisation:
+ *   nkv_block_dot2(Q, j, x=q_{j-1}, y=f, NKV_X_IS_LAST) -> h; all-reduce 2j
+ *   nkv_mgs_icwy_solve(j, G, ldg, h, h+j, h1)                  (pass-1 coefficients)
+ *   nkv_block_update_dot(Q, j, h1, f, h2); all-reduce j      (f -= Q h1; h2 = Q^T W f)
+ *   nkv_mgs_icwy_solve(j, G, ldg, NULL, h2, h2)              (pass-2 coefficients)
+ *   nkv_block_update(Q, j, h2, f, nrm, NKV_NORM2); all-reduce 1; nkv_arnoldi_finish(f, nrm, ...) */
+int nkv_mgs_icwy_solve(int j, double* G, int64_t ldg, const double* grow, const double* b, double* x,
+                       void* stream);
 
 /* ---- svds: Golub–Kahan–Lanczos with delayed re-orthogonalisation (f1; LightKrylov svds as called by
  * transient_growth_analysis / resolvent_analysis, linear_stab.f90:112,153).  Two bases U, V, each

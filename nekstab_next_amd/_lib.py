@@ -86,6 +86,7 @@ _SIGNATURES = {
     "nkv_arnoldi_finish": (c_int, [_L, _P, _P, _P, c_int, _P, _P, _P, c_uint, _P]),
     "nkv_block_dot2": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_dcgs2_coef": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, _P]),
+    "nkv_mgs_icwy_solve": (c_int, [c_int, _P, c_int64, _P, _P, _P, _P]),
     "nkv_dcgs2_update": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, _P, _P, c_uint, _P]),
     "nkv_arnoldi_scratch_doubles": (c_size_t, [c_int]),
     "nkv_arnoldi_dcgs2": (c_int, [_L, _P, _P, c_int, c_int, _P, c_int64, _P, _P, _P, MATVEC_FN, _P, ALLREDUCE_FN, _P,

@@ -32,6 +32,14 @@ Two orthogonalisation modes share the rest of the path:
   the reference's ``update_hessenberg_matrix`` entry), the all-reduce as a callback.
 * ``"mgs2"`` (reference operation order, for parity studies): the reference's two sequential
   MGS passes, one weighted dot + all-reduce + axpy per column.
+* ``"mgs2-icwy"``: the same two MGS passes in inverse compact WY form (Świrydowicz et al. 2020):
+  each pass's coefficients come from the classical dots b = Q^T W f through alpha = (I + L)^{-1} b,
+  L the strictly lower part of the basis's Gram matrix (kept on the device, one row per step from
+  the step's own two-vector multi-dot), so a step reads Q three times, like ``"cgs2"``.  Equal to
+  MGS in exact arithmetic for ANY basis, which is what the reference's non-orthonormal bases need
+  (the unnormalised noise/load seed, eigensolvers.f90:192-223; a restart with time in k_dot), where
+  classical Gram–Schmidt gives a different factorisation.  Whole factorisations only
+  (``arnoldi_factorization``): the Gram rows of the columns before ``mstart`` are rebuilt first.
 
 No step synchronises the host: H lives on the device until the factorisation ends.
 """
@@ -82,6 +90,9 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
     projection coefficients h1+h2 go to hcol[0:j] and ||f|| to hcol[j] (device memory).  j = 0
     only normalises."""
     w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    if mode == "mgs2-icwy":
+        raise ValueError("mode 'mgs2-icwy' keeps the basis's Gram matrix across steps: run it through "
+                         "arnoldi_factorization (or use 'mgs2' for a single step)")
     if mode in ("cgs2-native", "mgs2-native"):   # the cgs2 / mgs2 sequence as ONE library call
         scratch = _native_scratch(ctx, j)
         errors = []
@@ -135,7 +146,7 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         if tm:
             tm.begin("block_update")
         ctx.call("nkv_block_update", w, Q.ptr, j, h2.data_ptr(), f.ptr, nrm.data_ptr(), ws,
-                 NKV_TIME | NKV_NORM2 | tf, st)
+                 NKV_TIME | NKV_NORM2 | (NKV_TIME_DOT if tf else 0), st)
         if tm:
             tm.end("block_update", b_upd + 8.0 * lay.n_v)
         ctx.comm.allreduce_(nrm)
@@ -273,6 +284,63 @@ def _dcgs2_close_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> N
     ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
 
 
+def _icwy_gram(ctx: NekContext, Q: Basis, mstart: int) -> torch.Tensor:
+    """The row-major Gram matrix of ``"mgs2-icwy"`` (kept on the context, ld = max_cols + 1), with
+    the rows of columns 1..mstart-2 rebuilt from the basis as it stands (after a restart the kept
+    columns are new vectors; row mstart-1 comes from the first step's own multi-dot)."""
+    ldg = ctx.max_cols + 1
+    G = getattr(ctx, "_icwy_G", None)
+    if G is None:
+        G = ctx._icwy_G = torch.zeros((ldg, ldg), dtype=torch.float64, device=ctx.device)
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    for i in range(1, mstart - 1):
+        ctx.call("nkv_block_dot", w, Q.ptr, i, Q.col_ptr(i), G[i].data_ptr(), ws, tf, st)
+        ctx.comm.allreduce_(G[i, :i])
+    return G
+
+
+def _icwy_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, G: torch.Tensor) -> None:
+    """Step j (1-based) of ``"mgs2-icwy"``: f = A q_{j-1} is orthogonalised against Q[0:j] by two MGS
+    passes in inverse compact WY form; Q[j] = f/||f||, H column j-1 = alpha_1 + alpha_2, ||f||."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    ldg = G.shape[1]
+    h = ctx.hd[: 2 * j]
+    hp, gp = h.data_ptr(), G.data_ptr()
+    h1, h2, nrm = ctx.h1[:j], ctx.h2[:j], ctx.scal[3:4]
+    if tm:
+        tm.begin("block_dot2")
+    # [Q^T W q_{j-1} (the Gram row of the newest column) ; Q^T W f (pass-1 classical dots)]
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, Q.col_ptr(j - 1), f.ptr, hp, ws, tf | NKV_X_IS_LAST, st)
+    if tm:
+        tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    ctx.call_nl("nkv_mgs_icwy_solve", j, gp, ldg, hp, hp + 8 * j, h1.data_ptr(), st)
+    b_upd = 8.0 * (j * lay.N + 2 * lay.N)
+    if tm:
+        tm.begin("update_dot")
+    ctx.call("nkv_block_update_dot", w, Q.ptr, j, h1.data_ptr(), f.ptr, h2.data_ptr(), ws,
+             NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
+    if tm:
+        tm.end("update_dot", b_upd + 8.0 * lay.n_v)
+    ctx.comm.allreduce_(h2)
+    ctx.call_nl("nkv_mgs_icwy_solve", j, gp, ldg, None, h2.data_ptr(), h2.data_ptr(), st)
+    if tm:
+        tm.begin("block_update")
+    ctx.call("nkv_block_update", w, Q.ptr, j, h2.data_ptr(), f.ptr, nrm.data_ptr(), ws, NKV_TIME | NKV_NORM2 | (NKV_TIME_DOT if tf else 0), st)
+    if tm:
+        tm.end("block_update", b_upd + 8.0 * lay.n_v)
+    ctx.comm.allreduce_(nrm)
+    if tm:
+        tm.begin("finish")
+    ctx.call("nkv_arnoldi_finish", f.ptr, nrm.data_ptr(), Q.col_ptr(j), j, h1.data_ptr(), h2.data_ptr(),
+             Hd.col_ptr(j - 1), 0, st)
+    if tm:
+        tm.end("finish", 16.0 * lay.N)
+
+
 def _native_scratch(ctx: NekContext, m: int) -> torch.Tensor:
     """Device scratch of the one-call drivers (nkv_arnoldi_scratch_doubles), kept on the context."""
     need = int(ctx.lib.nkv_arnoldi_scratch_doubles(max(int(m), ctx.max_cols)))
@@ -391,6 +459,17 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
                 on_step(mstep - 1)
         _dcgs2_close(ctx, Q, Hd, mend)
         on_step(mend)
+        return
+    if mode == "mgs2-icwy":
+        if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+            raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        _settle_basis(Q, mstart, lazy=False)
+        G = _icwy_gram(ctx, Q, mstart)
+        for mstep in range(mstart, mend + 1):
+            (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
+            _icwy_step(ctx, Q, Hd, mstep, f, G)
+            if on_step is not None:
+                on_step(mstep)
         return
     if mode in ("cgs2-native", "mgs2-native") and on_step is None:   # per-column modes, one ABI call
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:

@@ -13,6 +13,7 @@ class KrylovSchurConfig:
     maxmodes: int = 20        # max eigenmodes exported (:13)
     mode: str = "dcgs2"       # "dcgs2" (block CGS2, delayed re-orth.: 2 reads of Q per step, the MI355X
     #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order);
+    #                           | "mgs2-icwy" (MGS in inverse compact WY form, 3 reads);
     #                           "dcgs2-native" | "cgs2-native" | "mgs2-native": the same sequences driven
     #                           by the library's one-call entry points (bit-identical)
     seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "load" (a
@@ -23,6 +24,10 @@ class KrylovSchurConfig:
     lazy_basis: bool = False       # dcgs2: leave finished columns as Q = S T (one vector write less per
     #                                step; the restart folds T in, the result basis is materialised once;
     #                                measured +0.3 % at N=1e8, m=128 -- DESIGN.md §6)
+    nonorth_mode: str = "mgs2-icwy"   # Gram–Schmidt where the basis is not orthonormal (noise/load seed,
+    #                                time in k_dot after a restart), which must be modified G-S as the
+    #                                reference's: "mgs2-icwy" (inverse compact WY form, 3 reads of Q
+    #                                per step) or "mgs2" (the reference's own per-column order)
     breakdown_tol: float = 1e-8    # |H(c+1,c)| < tol * ||H(1:c+2,c)||: the Krylov space became invariant;
     #                                that factorisation is redone in the reference's MGS2 order
 

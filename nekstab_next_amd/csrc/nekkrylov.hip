@@ -2084,8 +2084,10 @@ int nkv_block_update(const nkv_layout* L, const double* w, const double* Q, int 
     if (use_large_tiles(L)) CHECK(launch_block_update_p<NKV_PAIRS>(L, w, Q, j, h_dev, f, part, flags, st, &g));
     else CHECK(launch_block_update_p<NKV_PAIRS_SMALL>(L, w, Q, j, h_dev, f, part, flags, st, &g));
     if (norm) {
-        // ||f||^2 time term: (uparam(1)==2.1 / real_dot) only on the rank owning the replicated scalar
-        const bool tdot = (flags & NKV_TIME) && L->rank0;
+        // ||f||^2 time term (NKV_TIME_DOT: uparam(1)==2.1 / real_dot) only on the rank owning the
+        // replicated scalar.  NKV_TIME alone updates the slot but keeps it out of the norm (k_norm
+        // without the time product, krylov_subspace.f90:52-54).
+        const bool tdot = (flags & NKV_TIME_DOT) && L->rank0;
         hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(kThreads), 0, st, part, g, nrm2_dev,
                            tdot ? f + T : nullptr, (int64_t)0, tdot ? f + T : nullptr, nullptr, 1 << 30, nan_flag_of(ws));
         NKV_LAUNCHED();
@@ -2226,6 +2228,41 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     hipLaunchKernelGGL(k_reduce_cols, dim3(2 * j), dim3(kThreads), 0, st, part, tpf > 0 ? B : 0, h_dev,
                        tdot ? Q + T : nullptr, L->ld, tdot ? x + T : nullptr, tdot ? y + T : nullptr, j,
                        nan_flag_of(ws));
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+// MGS pass coefficients in inverse compact WY form (nkv_mgs_icwy_solve): x = (I + L)^{-1} b by
+// column sweeps, L the strictly lower part of the row-major Gram matrix G.  One workgroup; x lives
+// in LDS; sweep k subtracts G(i,k) x_k from every x_i, i > k (one barrier per column), so x_i
+// accumulates its terms in the order k = 0, 1, ... (fixed: the result does not depend on timing).
+// Row j-1 is taken from grow when given (and stored into G for the next steps).
+__global__ __launch_bounds__(kThreads) void k_mgs_icwy_solve(int j, double* __restrict__ G, int64_t ldg,
+                                                             const double* __restrict__ grow,
+                                                             const double* b, double* x) {
+    extern __shared__ double xs[];
+    for (int i = threadIdx.x; i < j; i += kThreads) xs[i] = b[i];
+    if (grow)
+        for (int k = threadIdx.x; k < j - 1; k += kThreads) G[(int64_t)(j - 1) * ldg + k] = grow[k];
+    for (int k = 0; k + 1 < j; ++k) {
+        __syncthreads();
+        const double xk = xs[k];
+        for (int i = k + 1 + threadIdx.x; i < j; i += kThreads) {
+            const double g = (grow && i == j - 1) ? grow[k] : G[(int64_t)i * ldg + k];
+            xs[i] = xs[i] - g * xk;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < j; i += kThreads) x[i] = xs[i];
+}
+
+int nkv_mgs_icwy_solve(int j, double* G, int64_t ldg, const double* grow, const double* b, double* x,
+                       void* stream) {
+    if (j < 1 || j > NKV_MAX_COLS) return fail(NKV_EINVAL, "icwy: j=%d outside 1..%d", j, NKV_MAX_COLS);
+    if (!G || !b || !x) return fail(NKV_EINVAL, "icwy: G/b/x is NULL");
+    if (ldg < j) return fail(NKV_EINVAL, "icwy: ldg=%lld < j=%d", (long long)ldg, j);
+    hipLaunchKernelGGL(k_mgs_icwy_solve, dim3(1), dim3(kThreads), j * sizeof(double), S(stream), j, G, ldg, grow,
+                       b, x);
     NKV_LAUNCHED();
     return NKV_OK;
 }
@@ -2561,7 +2598,7 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
     CHECK(reduce(h1, j, "first projection"));
     CHECK(nkv_block_update_dot(L, w, Q, j, h1, f, h2, ws, NKV_TIME | (tf ? NKV_TIME_DOT : 0u), stream));
     CHECK(reduce(h2, j, "second projection"));
-    CHECK(nkv_block_update(L, w, Q, j, h2, f, nrm, ws, NKV_TIME | NKV_NORM2 | tf, stream));
+    CHECK(nkv_block_update(L, w, Q, j, h2, f, nrm, ws, NKV_TIME | NKV_NORM2 | (tf ? NKV_TIME_DOT : 0u), stream));
     CHECK(reduce(nrm, 1, "norm"));
     return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
 }

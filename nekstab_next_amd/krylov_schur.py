@@ -57,6 +57,16 @@ def _mgs2_of(mode: str) -> str:
     return "mgs2-native" if mode.endswith("-native") else "mgs2"
 
 
+def _nonorth_of(mode: str, cfg: KrylovSchurConfig) -> str:
+    """The mode for a basis that is not orthonormal (``cfg.nonorth_mode``; "mgs2" keeps a native
+    mode's library-driven variant)."""
+    if cfg.nonorth_mode == "mgs2":
+        return _mgs2_of(mode)
+    if cfg.nonorth_mode != "mgs2-icwy":
+        raise ValueError(f"nonorth_mode={cfg.nonorth_mode!r}: 'mgs2-icwy' or 'mgs2'")
+    return cfg.nonorth_mode
+
+
 def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float, offset: int = 1) -> int:
     """First Arnoldi column c in [c0, k) whose new direction vanished (|H(c+1,c)| < tol ||H(0:c+2,c)||,
     the Krylov space is invariant to rounding), or that holds a non-finite entry; -1 if none.
@@ -186,8 +196,10 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # the "noise" seed leaves Q(1) unnormalised (eigensolvers.f90:195-203); the reference's MGS2
     # then projects against it as it stands, so its basis is not orthonormal (a projection onto an
     # unnormalised vector removes only part of the component) and classical and modified
-    # Gram–Schmidt no longer agree.  That mode therefore runs the reference's own operation order.
-    mode = "mgs2" if (cfg.seed_mode in ("noise", "load") and start is None) else cfg.mode
+    # Gram–Schmidt no longer agree.  That mode therefore runs modified Gram–Schmidt: by default in
+    # inverse compact WY form (the same coefficients, three reads of Q per step), or in the
+    # reference's own operation order (cfg.nonorth_mode = "mgs2").
+    mode = _nonorth_of(cfg.mode, cfg) if (cfg.seed_mode in ("noise", "load") and start is None) else cfg.mode
     if mode != cfg.mode:
         graphs, lazy = None, False
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)
@@ -238,8 +250,8 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         if ctx.time_in_dot and mode not in _MGS2:
             # the restart moves the fields but not `time` (eigensolvers.f90:421-432, 458-459), so
             # with time in k_dot (uparam(1)==2.1) the kept basis is no longer orthonormal: from here
-            # on the reference's MGS2 order is mirrored (CGS2/DCGS2 assume an orthonormal basis)
-            mode, graphs, lazy = _mgs2_of(mode), None, False
+            # on modified Gram–Schmidt is mirrored (CGS2/DCGS2 assume an orthonormal basis)
+            mode, graphs, lazy = _nonorth_of(mode, cfg), None, False
         res.mstart_history.append(mstart)
         res.selected_history.append(selected)
         Hd.upload(H)

@@ -544,14 +544,16 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
     np.testing.assert_allclose(hout.cpu().numpy(), href, rtol=1e-12, atol=1e-12 * np.abs(href).max())
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2"])
-def test_arnoldi_with_time_component_vs_oracle(gpu, mode):
-    """uparam(1)==2.1: the scalar `time` enters k_dot (krylov_subspace.f90:52-54) and follows every
-    update; the operator propagates it (time_scale)."""
+@pytest.mark.parametrize("time_dot", [True, False])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "cgs2-native", "mgs2-native"])
+def test_arnoldi_with_time_component_vs_oracle(gpu, mode, time_dot):
+    """The scalar `time` follows every update and the operator propagates it (time_scale); with
+    uparam(1)==2.1 it also enters k_dot (krylov_subspace.f90:52-54), otherwise it is carried but
+    kept out of every dot and norm (round 3: the CGS2 norm pass used to add it regardless)."""
     lay = LAYOUTS["3d_scalar"]
     w = syn.mass_weights(lay)
-    ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=True)
-    L = olayout(lay, time_in_dot=True)
+    ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=time_dot)
+    L = olayout(lay, time_in_dot=time_dot)
     d, _ = syn.diag_spectrum(lay)
     op = DiagOperator(ctx, d, time_scale=0.7)
     m = 12
@@ -573,6 +575,85 @@ def test_arnoldi_with_time_component_vs_oracle(gpu, mode):
     times = Q.storage.cpu().numpy()[:, lay.time_offset]
     np.testing.assert_allclose(times, Qr[:, -1], rtol=1e-10, atol=1e-14)
     assert np.any(np.abs(times) > 1e-3)  # the time component is really carried
+
+
+@pytest.mark.parametrize("time_dot", [False, True])
+@pytest.mark.parametrize("scale", [0.05, 1.0, 7.0])
+def test_mgs2_icwy_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
+    """"mgs2-icwy" (MGS in inverse compact WY form, nkv_mgs_icwy_solve) on the reference's
+    non-orthonormal bases: Q(1) NOT normalised (the noise/load seed leaves ||Q(1)|| = ||A s|| != 1,
+    eigensolvers.f90:192-223), where classical Gram–Schmidt is a different algorithm.  H and the
+    basis against the oracle's MGS2 in the reference's operation order (krylov_decomposition.f90:
+    155-186), 12 steps: H to 1e-12 of max|H|, columns to 1e-11; the same factorisation split in two
+    calls (the Gram rows of columns before mstart rebuilt by multi-dots) agrees with the single call
+    to 1e-13; CGS2 on the same basis is measurably different (so the test can tell the algorithms
+    apart)."""
+    lay = LAYOUTS["3d_scalar"]
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=time_dot)
+    L = olayout(lay, time_in_dot=time_dot)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d, time_scale=0.7)
+    m = 12
+    q0 = syn.hash_vector(lay, 7)
+    q0[lay.time_offset] = 0.3
+    q0r = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, q0r)
+    q0r *= scale
+    q0 = syn.from_reference_order(lay, q0r)
+    Qr = np.zeros((m + 1, L.len))
+    Qr[0] = q0r
+    Hr = np.zeros((m + 1, m))
+    dref = syn.to_reference_order(lay, d)
+    orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
+    out = {}
+    for name, mode, splits in (("one", "mgs2-icwy", [(1, m)]), ("split", "mgs2-icwy", [(1, 5), (6, m)]),
+                               ("cgs2", "cgs2", [(1, m)])):
+        Q = ctx.basis(m + 1)
+        Q[0].from_packed(q0)
+        Hd = HessenbergDev(ctx, m)
+        for a, b in splits:
+            arnoldi_factorization(ctx, op, Q, Hd, a, b, mode=mode)
+        ctx.check_nan()
+        out[name] = (Hd.download(), np.stack([syn.to_reference_order(lay, Q[i].to_packed()) for i in range(m + 1)]))
+    H, Qg = out["one"]
+    hmax = np.max(np.abs(Hr))
+    assert np.max(np.abs(H - Hr)) <= 1e-12 * hmax, np.max(np.abs(H - Hr)) / hmax
+    np.testing.assert_allclose(Qg, Qr, rtol=0, atol=1e-11 * max(1.0, scale))
+    assert np.max(np.abs(out["split"][0] - H)) <= 1e-13 * hmax
+    if scale != 1.0:
+        assert np.max(np.abs(out["cgs2"][0] - Hr)) > 1e-6 * hmax
+
+
+def test_mgs2_icwy_solve_entry(gpu):
+    """nkv_mgs_icwy_solve alone: x = (I + L)^{-1} b for a random row-major Gram matrix (the new row
+    from grow, stored into G), in place, against numpy's triangular solve; argument checks."""
+    from nekstab_next_amd import _lib as lib_mod
+
+    lib = lib_mod.load()
+    st = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(3)
+    for j in (1, 2, 7, 64, 257):
+        ldg = j + 3
+        Gh = rng.standard_normal((ldg, ldg)) * (0.5 / j)   # a near-orthonormal basis's Gram entries
+        grow = rng.standard_normal(max(j - 1, 1)) * (0.5 / j)
+        b = rng.standard_normal(j)
+        G = torch.as_tensor(Gh).cuda()
+        gr = torch.as_tensor(grow).cuda()
+        x = torch.as_tensor(b).cuda()
+        lib_mod.check(lib.nkv_mgs_icwy_solve(j, G.data_ptr(), ldg, gr.data_ptr(), x.data_ptr(), x.data_ptr(), st), "icwy")
+        torch.cuda.synchronize()
+        Lm = np.tril(Gh[:j, :j], -1)
+        if j > 1:
+            Lm[j - 1, : j - 1] = grow[: j - 1]
+        ref = np.linalg.solve(np.eye(j) + Lm, b)
+        np.testing.assert_allclose(x.cpu().numpy(), ref, rtol=1e-10, atol=1e-12)
+        if j > 1:
+            np.testing.assert_array_equal(G.cpu().numpy()[j - 1, : j - 1], grow[: j - 1])
+    G = torch.zeros((4, 4), dtype=torch.float64, device="cuda")
+    assert lib.nkv_mgs_icwy_solve(0, G.data_ptr(), 4, None, G.data_ptr(), G.data_ptr(), st) != 0
+    assert lib.nkv_mgs_icwy_solve(5, G.data_ptr(), 4, None, G.data_ptr(), G.data_ptr(), st) != 0
+    assert lib.nkv_mgs_icwy_solve(2, None, 4, None, G.data_ptr(), G.data_ptr(), st) != 0
 
 
 def test_empty_shard(gpu):

@@ -420,9 +420,12 @@ def test_krylov_schur_knobs(gpu):
     orc.k_normalize(L, w, sn)
     q1 = np.zeros(L.len)
     orc.lib().orc_op_diag(ctypes.byref(L.c), dref, sn, q1, 0.0)
-    res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise"))
     ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
-    _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
+    for nonorth in ("mgs2-icwy", "mgs2"):   # MGS in inverse compact WY form (default) / reference order
+        res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise",
+                                                            nonorth_mode=nonorth))
+        _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
+        assert res.schur_cnt >= 1 and not res.breakdowns
     # as_is: the caller's vector is the first basis vector
     q1 = orc.prepare_seed(L, w, s_ref)
     seed2 = ctx.vector().from_packed(syn.from_reference_order(lay, q1))
@@ -446,8 +449,9 @@ def test_krylov_schur_knobs(gpu):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
 
 
+@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2"])
 @pytest.mark.parametrize("transpose", [False, True])
-def test_krylov_schur_load_seed_vs_oracle(gpu, tmp_path, transpose):
+def test_krylov_schur_load_seed_vs_oracle(gpu, tmp_path, transpose, nonorth):
     """ifseed_load (eigensolvers.f90:210-223): mode 1's real part of an earlier run, dRe (direct) or
     aRe (adjoint) <session>0.f00001, written by the oracle's independent #std writer; the product
     reads it (load_seed), k_normalizes it and applies one matvec (seed_mode "load").  The oracle
@@ -466,7 +470,8 @@ def test_krylov_schur_load_seed_vs_oracle(gpu, tmp_path, transpose):
     for prefix, s in (("dRe", 11), ("aRe", 12)):
         nekio.write_std(str(tmp_path / f"{prefix}cyl0.f00001"), g, syn.to_reference_order(lay, syn.hash_vector(lay, s)))
     seed = load_seed(ctx, str(tmp_path), "cyl", transpose=transpose)
-    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="load"),
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed,
+                       KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="load", nonorth_mode=nonorth),
                        transpose=transpose)
     s_ref = nekio.read_std_vector([str(tmp_path / f"{'aRe' if transpose else 'dRe'}cyl0.f00001")], g)
     np.testing.assert_allclose(syn.to_reference_order(lay, seed.to_packed()), s_ref, rtol=0, atol=1e-13)
@@ -514,8 +519,9 @@ def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
     assert np.sqrt(np.sum(np.tile(w, L.nwf) * diff * diff)) < 1e-10
 
 
+@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2"])
 @pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
-def test_krylov_schur_time_component_with_restarts(gpu, mode):
+def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     """uparam(1)==2.1 (the time slot inside k_dot) through Krylov–Schur restarts: the restart
     rotation and Q(mstart) <- Q(k+1) move the fields only, not time (eigensolvers.f90:421-432,
     458-459), as the oracle does; restart trajectory and Ritz values match it (1e-10).  The seed
@@ -530,7 +536,7 @@ def test_krylov_schur_time_component_with_restarts(gpu, mode):
     q0[-1] = 0.3
     orc.k_normalize(L, w, q0)
     seed = ctx.vector().from_packed(syn.from_reference_order(lay, q0))
-    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, mode=mode, seed_mode="as_is")
+    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, mode=mode, seed_mode="as_is", nonorth_mode=nonorth)
     res = krylov_schur(ctx, op, seed, cfg)
     dref = syn.to_reference_order(lay, d)
     ref = orc.krylov_schur(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), q0, 16, 5)
