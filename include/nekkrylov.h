@@ -386,6 +386,19 @@ int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const 
 int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
                   double* out, int ncomp, void* stream);
 
+/* ---- seeds (utils.f90:258-418; the noise seed is the reference's default, main.f90:29) ---------
+ * nkv_mth_rand_add: one weighted field q (n_v points, Nek point order) += mth_rand(il, jl, kl, ieg,
+ * xl, fc) (utils.f90:408-418), the pointwise part of op_add_noise (fc per velocity component,
+ * :321-331) and add_noise_scal (:258-295); xm/ym/zm are this rank's GLL coordinates (n_v each; zm
+ * exactly when lz1 > 1), e_first the 0-based global number of its first element (ieg = e_first+e+1).
+ * nkv_group_average: q[m] <- mean of q over m's group, for CSR groups of coincident points
+ * (start: n_groups+1 offsets, members: point indices; device arrays) — dssum followed by vmult on
+ * one rank (:339-340). */
+int nkv_mth_rand_add(const nkv_layout* L, int lx1, int ly1, int lz1, int64_t e_first, const double* xm,
+                     const double* ym, const double* zm, double fc1, double fc2, double fc3, double* q,
+                     void* stream);
+int nkv_group_average(int64_t n_groups, const int64_t* start, const int64_t* members, double* q, void* stream);
+
 /* ---- ts_gmres host helper (a17, newton_krylov.f90:250-269) -------------------------------
  * The least-squares residual ||beta e_1 - H(1:k+2, 1:k+1) y|| after one more Hessenberg column, in
  * O(k) host work (Givens rotations; no device work, no stream).  h: H(0:k+1, k) (0-based column k,

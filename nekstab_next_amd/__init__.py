@@ -15,7 +15,7 @@ def __getattr__(name):
     import importlib
 
     for mod in ("vector", "operators", "arnoldi", "krylov_schur", "gmres", "newton", "sensitivity", "lapack",
-                "comm", "synthetic", "lightkrylov", "drivers", "checkpoint", "fld", "boostconv", "_lib"):
+                "comm", "synthetic", "lightkrylov", "drivers", "checkpoint", "fld", "boostconv", "seeds", "_lib"):
         if name == mod:
             return importlib.import_module(f".{mod}", __name__)
     raise AttributeError(name)

@@ -3022,6 +3022,187 @@ int nkv_fill_hash(const nkv_layout* L, double* x, uint64_t seed, int64_t v_offse
     return NKV_OK;
 }
 
+// ---- correctly rounded sin / cos (the seed hash only) ----------------------------------------
+// mth_rand's cos(1e3 sin(1e3 sin r)) turns one unit in the last place of a sin into ~1e-3 of noise,
+// so the device hash equals the reference's (gfortran + glibc libm, which rounds sin/cos correctly
+// in all but rare cases) only if its sin/cos round correctly too: double-double range reduction
+// by pi/2 in four parts (|k| < 2^53) and double-double Taylor series on |r| <= pi/4 (~2^-100
+// relative), rounded once to double.  Not used on any solver path.
+struct nkv_dd { double hi, lo; };
+__device__ __forceinline__ nkv_dd dd_two_sum(double a, double b) {
+#pragma clang fp contract(off)
+    const double s = a + b, bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ nkv_dd dd_fast(double a, double b) {
+#pragma clang fp contract(off)
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+__device__ __forceinline__ nkv_dd dd_add(nkv_dd a, nkv_dd b) {
+#pragma clang fp contract(off)
+    nkv_dd s = dd_two_sum(a.hi, b.hi);
+    const nkv_dd t = dd_two_sum(a.lo, b.lo);
+    s = dd_fast(s.hi, s.lo + t.hi);
+    return dd_fast(s.hi, s.lo + t.lo);
+}
+__device__ __forceinline__ nkv_dd dd_mul(nkv_dd a, nkv_dd b) {
+#pragma clang fp contract(off)
+    const double p = a.hi * b.hi;
+    const double e = fma(a.hi, b.hi, -p);
+    return dd_fast(p, e + (a.hi * b.lo + a.lo * b.hi));
+}
+__device__ __forceinline__ nkv_dd dd_prod(double a, double b) {   // exact
+    const double p = a * b;
+    return {p, fma(a, b, -p)};
+}
+__device__ const double kNkvSinC[15][2] = {
+    {0x1.0000000000000p+0, 0x0.0p+0},
+    {-0x1.5555555555555p-3, -0x1.5555555555555p-57},
+    {0x1.1111111111111p-7, 0x1.1111111111111p-63},
+    {-0x1.a01a01a01a01ap-13, -0x1.a01a01a01a01ap-73},
+    {0x1.71de3a556c734p-19, -0x1.c154f8ddc6c00p-73},
+    {-0x1.ae64567f544e4p-26, 0x1.c062e06d1f209p-80},
+    {0x1.6124613a86d09p-33, 0x1.f28e0cc748ebep-87},
+    {-0x1.ae7f3e733b81fp-41, -0x1.1d8656b0ee8cbp-97},
+    {0x1.952c77030ad4ap-49, 0x1.ac981465ddc6cp-103},
+    {-0x1.2f49b46814157p-57, -0x1.2650f61dbdcb4p-112},
+    {0x1.71b8ef6dcf572p-66, -0x1.d043ae40c4647p-120},
+    {-0x1.761b41316381ap-75, 0x1.3423c7d91404fp-130},
+    {0x1.3f3ccdd165fa9p-84, -0x1.58ddadf344487p-139},
+    {-0x1.d1ab1c2dccea3p-94, -0x1.054d0c78aea14p-149},
+    {0x1.259f98b4358adp-103, 0x1.eaf8c39dd9bc5p-157},
+};
+__device__ const double kNkvCosC[16][2] = {
+    {0x1.0000000000000p+0, 0x0.0p+0},
+    {-0x1.0000000000000p-1, 0x0.0p+0},
+    {0x1.5555555555555p-5, 0x1.5555555555555p-59},
+    {-0x1.6c16c16c16c17p-10, 0x1.f49f49f49f49fp-65},
+    {0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-76},
+    {-0x1.27e4fb7789f5cp-22, -0x1.cbbc05b4fa99ap-76},
+    {0x1.1eed8eff8d898p-29, -0x1.2aec959e14c06p-83},
+    {-0x1.93974a8c07c9dp-37, -0x1.05d6f8a2efd1fp-92},
+    {0x1.ae7f3e733b81fp-45, 0x1.1d8656b0ee8cbp-101},
+    {-0x1.6827863b97d97p-53, -0x1.eec01221a8b0bp-107},
+    {0x1.e542ba4020225p-62, 0x1.ea72b4afe3c2fp-120},
+    {-0x1.0ce396db7f853p-70, 0x1.aebcdbd20331cp-124},
+    {0x1.f2cf01972f578p-80, -0x1.9ada5fcc1ab14p-135},
+    {-0x1.88e85fc6a4e5ap-89, 0x1.71c37ebd16540p-143},
+    {0x1.0a18a2635085dp-98, 0x1.b9e2e28e1aa54p-153},
+    {-0x1.3932c5047d60ep-108, -0x1.832b7b530a627p-162},
+};
+
+// quadrant k mod 4 and r = x - k pi/2 as a double-double
+__device__ __forceinline__ int dd_reduce(double x, nkv_dd* r) {
+#pragma clang fp contract(off)
+    const double k = rint(x * 0x1.45f306dc9c883p-1);   // x * 2/pi
+    nkv_dd t = dd_add({x, 0.0}, dd_prod(-k, 0x1.921fb54442d18p+0));
+    t = dd_add(t, dd_prod(-k, 0x1.1a62633145c07p-54));
+    t = dd_add(t, dd_prod(-k, -0x1.f1976b7ed8fbcp-110));
+    t = dd_add(t, dd_prod(-k, 0x1.4cf98e804177dp-164));
+    *r = t;
+    return (int)(((int64_t)k) & 3);
+}
+__device__ __forceinline__ nkv_dd dd_sin_r(nkv_dd r) {   // |r| <= ~pi/4
+    const nkv_dd z = dd_mul(r, r);
+    nkv_dd p = {kNkvSinC[14][0], kNkvSinC[14][1]};
+    for (int i = 13; i >= 0; --i) p = dd_add(dd_mul(p, z), {kNkvSinC[i][0], kNkvSinC[i][1]});
+    return dd_mul(p, r);
+}
+__device__ __forceinline__ nkv_dd dd_cos_r(nkv_dd r) {
+    const nkv_dd z = dd_mul(r, r);
+    nkv_dd p = {kNkvCosC[15][0], kNkvCosC[15][1]};
+    for (int i = 14; i >= 0; --i) p = dd_add(dd_mul(p, z), {kNkvCosC[i][0], kNkvCosC[i][1]});
+    return p;
+}
+__device__ double cr_sin(double x) {
+    if (!(fabs(x) < 0x1p50)) return sin(x);   // not reached by the hash (|x| < 1e10)
+    nkv_dd r;
+    const int q = dd_reduce(x, &r);
+    const nkv_dd v = (q & 1) ? dd_cos_r(r) : dd_sin_r(r);
+    const double s = v.hi + v.lo;
+    return (q & 2) ? -s : s;
+}
+__device__ double cr_cos(double x) {
+    if (!(fabs(x) < 0x1p50)) return cos(x);
+    nkv_dd r;
+    const int q = dd_reduce(x, &r);
+    const nkv_dd v = (q & 1) ? dd_sin_r(r) : dd_cos_r(r);
+    const double c = v.hi + v.lo;
+    return ((q + 1) & 2) ? -c : c;
+}
+
+// Seed noise of op_add_noise / add_noise_scal (utils.f90:258-359): q[p] += mth_rand(il, jl, kl, ieg,
+// xl, fc) (utils.f90:408-418) at every point p of one weighted field, in Nek's point order (il fastest)
+// with ieg = e_first + e + 1 the global element number:
+//   r = fc1 (ieg + x sin y) + fc2 il jl + fc3 il;   3-D: r = fc1 (ieg + z sin r) + fc2 kl il + fc3 kl
+//   mth_rand = cos(1e3 sin(1e3 sin r))
+// evaluated in the reference's operand order with no contraction, every sin / cos correctly rounded
+// (cr_sin / cr_cos above).  The hash amplifies the last bit of every sin by ~1e6, so the result
+// depends on the math library's rounding: it equals the formula with correctly rounded libm bit for
+// bit, and glibc's (which misrounds ~0.1 % of near-midpoint cases) at >99 % of the points.
+__global__ __launch_bounds__(kThreads) void k_mth_rand_add(int nx, int ny, int nz, int64_t n, int64_t e_first,
+                                                           const double* __restrict__ xm,
+                                                           const double* __restrict__ ym,
+                                                           const double* __restrict__ zm, double fc1, double fc2,
+                                                           double fc3, double* __restrict__ q) {
+#pragma clang fp contract(off)
+    const int64_t ppe = (int64_t)nx * ny * nz;
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kThreads) {
+        const int64_t e = p / ppe;
+        const int r = (int)(p - e * ppe);
+        const double il = (double)(r % nx + 1), jl = (double)((r / nx) % ny + 1), kl = (double)(r / (nx * ny) + 1);
+        const double ieg = (double)(e_first + e + 1);
+        double m = fc1 * (ieg + xm[p] * cr_sin(ym[p])) + fc2 * il * jl + fc3 * il;
+        if (zm) m = fc1 * (ieg + zm[p] * cr_sin(m)) + fc2 * kl * il + fc3 * kl;
+        q[p] = q[p] + cr_cos(1.0e3 * cr_sin(1.0e3 * cr_sin(m)));
+    }
+}
+
+// Direct-stiffness averaging on one rank (dssum then vmult, as op_add_noise applies to its noise,
+// utils.f90:339-340): every point of a group of coincident GLL points (CSR: members[start[g] ..
+// start[g+1])) gets the group's mean, summed in member order.  Singleton points keep their value.
+__global__ __launch_bounds__(kThreads) void k_group_average(int64_t n_groups, const int64_t* __restrict__ start,
+                                                            const int64_t* __restrict__ members,
+                                                            double* __restrict__ q) {
+#pragma clang fp contract(off)
+    for (int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x; g < n_groups; g += (int64_t)gridDim.x * kThreads) {
+        const int64_t a = start[g], b = start[g + 1];
+        double s = 0.0;
+        for (int64_t i = a; i < b; ++i) s = s + q[members[i]];
+        const double v = s * (1.0 / (double)(b - a));
+        for (int64_t i = a; i < b; ++i) q[members[i]] = v;
+    }
+}
+
+int nkv_mth_rand_add(const nkv_layout* L, int lx1, int ly1, int lz1, int64_t e_first, const double* xm,
+                     const double* ym, const double* zm, double fc1, double fc2, double fc3, double* q,
+                     void* stream) {
+    CHECK(check_layout(L));
+    if (lx1 < 1 || ly1 < 1 || lz1 < 1 || L->n_v % ((int64_t)lx1 * ly1 * lz1) != 0)
+        return fail(NKV_EINVAL, "mth_rand: lx1*ly1*lz1=%d*%d*%d does not divide n_v=%lld", lx1, ly1, lz1,
+                    (long long)L->n_v);
+    if (e_first < 0) return fail(NKV_EINVAL, "mth_rand: e_first=%lld < 0", (long long)e_first);
+    if ((lz1 > 1) != (zm != nullptr)) return fail(NKV_EINVAL, "mth_rand: zm must be given exactly when lz1 > 1");
+    CHECK(check_ptr(xm, "xm"));
+    CHECK(check_ptr(ym, "ym"));
+    CHECK(check_ptr(q, "q"));
+    hipLaunchKernelGGL(k_mth_rand_add, dim3(grid_for(L->n_v)), dim3(kThreads), 0, S(stream), lx1, ly1, lz1, L->n_v,
+                       e_first, xm, ym, zm, fc1, fc2, fc3, q);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_group_average(int64_t n_groups, const int64_t* start, const int64_t* members, double* q, void* stream) {
+    if (n_groups < 0) return fail(NKV_EINVAL, "group_average: n_groups=%lld < 0", (long long)n_groups);
+    if (n_groups == 0) return NKV_OK;
+    if (!start || !members || !q) return fail(NKV_EINVAL, "group_average: start/members/q is NULL");
+    hipLaunchKernelGGL(k_group_average, dim3(grid_for(n_groups)), dim3(kThreads), 0, S(stream), n_groups, start,
+                       members, q);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
 int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
                   double* out, int ncomp, void* stream) {
     CHECK(check_layout(L));

@@ -1,0 +1,175 @@
+"""The reference's default seed vector of the eigensolvers: hash noise on the GLL mesh.
+
+References: ``prepare_seed`` (core/linear_stab.f90:243-293; the LightKrylov drivers) and the seed
+branches of ``krylov_schur`` (core/eigensolvers.f90:190-223), with ``ifseed_nois = .true.`` the
+default (core/main.f90:29); the noise is ``op_add_noise`` / ``add_noise_scal`` (core/utils.f90:
+258-359) over the hash ``mth_rand`` (:408-418).
+
+* the pointwise noise runs on the device (``nkv_mth_rand_add``), one weighted field per launch, from
+  this rank's GLL coordinates (``coords_from_fld``: the X block of any field file of the case);
+* Nek5000's ``dssum`` + ``vmult`` (direct-stiffness averaging of the points elements share) and
+  ``dsavg`` are restated on one rank from the coordinates (``FaceAverage``: groups of coincident
+  points, averaged on the device by ``nkv_group_average``).  On several ranks the points on a
+  shard boundary would need Nek's gather-scatter across ranks: pass your own ``face_average``;
+* ``bcdirVC`` / ``bcdirSC`` (Dirichlet masks: walls, inflow) need the case's boundary conditions,
+  which field files do not hold: pass them as ``mask`` (a vector of 0/1 multipliers, 1 elsewhere).
+
+The hash is ``cos(1e3 sin(1e3 sin r))`` with r ~ 1e7: one unit in the last place of any ``sin`` moves
+the result by up to ~1e-3, so the noise is reproducible only with the same math library rounding;
+the tests compare the device against glibc's (the reference's gfortran libm) point by point.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .vector import NekContext, NekVector
+
+# op_add_noise's per-component constants (utils.f90:324-331)
+NOISE_FC = ((3.0e4, -1.5e3, 0.5e5), (2.3e4, 2.3e3, -2.0e5), (2.0e4, 1.0e3, 1.0e5))
+# add_noise_scal's constants for the temperature (linear_stab.f90:260; eigensolvers.f90:196)
+SCAL_FC = (9.0e4, 3.0e3, 4.0e5)
+
+
+def coords_from_fld(lay, files) -> dict:
+    """This rank's GLL coordinates {"x", "y"[, "z"]} (n_v each, Nek point order) from field files
+    holding a mesh block (rdcode with X), mapped by their element map like ``vector_from_fld``."""
+    from . import fld
+
+    if isinstance(files, fld.FldFile):
+        files = [files]
+    e0, e1 = lay.elem_range()
+    names = ["x", "y", "z"][: lay.ldim]
+    out = {nm: np.zeros(lay.n_v) for nm in names}
+    seen = np.zeros(lay.nelv, dtype=bool)
+    for f in files:
+        if "x" not in f.fields:
+            continue
+        if f.nx != lay.lx1 or f.ldim != lay.ldim:
+            raise ValueError(f"field file is lx1={f.nx} ldim={f.ldim}, layout lx1={lay.lx1} ldim={lay.ldim}")
+        g = f.emap.astype(np.int64) - 1
+        sel = np.nonzero((g >= e0) & (g < e1))[0]
+        loc = g[sel] - e0
+        for nm in names:
+            out[nm].reshape(lay.nelv, lay.pts_v)[loc] = f.fields[nm][sel]
+        seen[loc] = True
+    if not np.all(seen):
+        raise ValueError(f"{int(np.count_nonzero(~seen))} local elements have no coordinates in the files")
+    return out
+
+
+def coincident_groups(coords: dict, rel_tol: float = 1e-9) -> tuple[np.ndarray, np.ndarray]:
+    """CSR groups (start, members) of the points with equal coordinates (to ``rel_tol`` of the mesh
+    extent), groups of two or more only — the points Nek5000's gather-scatter sums over."""
+    xs = [np.asarray(coords[k], dtype=np.float64) for k in ("x", "y", "z") if k in coords]
+    n = xs[0].size
+    if n == 0:
+        return np.zeros(1, np.int64), np.zeros(0, np.int64)
+    ext = max(float(np.ptp(x)) for x in xs) or 1.0
+    keys = [np.round(x / (rel_tol * ext)).astype(np.int64) for x in xs]
+    order = np.lexsort(keys[::-1])
+    ks = np.stack([k[order] for k in keys], axis=1)
+    new = np.ones(n, dtype=bool)
+    new[1:] = np.any(ks[1:] != ks[:-1], axis=1)
+    gid = np.cumsum(new) - 1
+    counts = np.bincount(gid)
+    multi = counts[gid] > 1
+    # lexsort is stable: inside a group the points stay in ascending order (the summation order)
+    members = order[multi].astype(np.int64)
+    g_multi = gid[multi]
+    starts = np.flatnonzero(np.r_[True, g_multi[1:] != g_multi[:-1]]) if members.size else np.zeros(0, np.int64)
+    return np.r_[starts, members.size].astype(np.int64), members
+
+
+class FaceAverage:
+    """``dssum`` then ``vmult`` (and ``dsavg``, the same again) on one rank: each group of coincident
+    points gets its mean (``nkv_group_average``)."""
+
+    def __init__(self, ctx: NekContext, coords: dict, rel_tol: float = 1e-9):
+        if ctx.comm.world > 1:
+            raise ValueError("FaceAverage averages one rank's points only; at world > 1 pass the case's own "
+                             "gather-scatter as face_average (shard-boundary points are shared across ranks)")
+        start, members = coincident_groups(coords, rel_tol)
+        self.ctx = ctx
+        self.n_groups = start.size - 1
+        self.start = torch.as_tensor(start).to(ctx.device)
+        self.members = torch.as_tensor(members if members.size else np.zeros(1, np.int64)).to(ctx.device)
+
+    def __call__(self, vec: NekVector, fields) -> None:
+        ctx, lay = self.ctx, self.ctx.layout
+        for f in fields:
+            ctx.call_nl("nkv_group_average", self.n_groups, self.start.data_ptr(), self.members.data_ptr(),
+                        vec.ptr + 8 * f * lay.sv, ctx.stream)
+
+
+def _coord_tensors(ctx: NekContext, coords: dict):
+    lay = ctx.layout
+    out = []
+    for k in ("x", "y", "z")[: lay.ldim]:
+        a = np.asarray(coords[k], dtype=np.float64)
+        if a.size != lay.n_v:
+            raise ValueError(f"coords[{k!r}]: {a.size} points, the layout has n_v={lay.n_v}")
+        out.append(torch.as_tensor(a).to(ctx.device) if lay.n_v else torch.zeros(2, dtype=torch.float64,
+                                                                                 device=ctx.device))
+    return out
+
+
+def mth_rand_add(ctx: NekContext, vec: NekVector, field: int, coords: dict, fc) -> None:
+    """vec's weighted field ``field`` += mth_rand(il, jl, kl, ieg, xl, fc) at every point
+    (utils.f90:408-418; ieg from this rank's element range)."""
+    lay = ctx.layout
+    if not 0 <= field < lay.n_wf:
+        raise ValueError(f"field {field} outside 0..{lay.n_wf - 1}")
+    ct = _coord_tensors(ctx, coords)
+    lz1 = lay.lx1 if lay.ldim == 3 else 1
+    ctx.call("nkv_mth_rand_add", lay.lx1, lay.lx1, lz1, lay.elem_range()[0], ct[0].data_ptr(), ct[1].data_ptr(),
+             ct[2].data_ptr() if lay.ldim == 3 else None, float(fc[0]), float(fc[1]), float(fc[2]),
+             vec.ptr + 8 * field * lay.sv, ctx.stream)
+
+
+def _finish(ctx: NekContext, vec: NekVector, fields, face_average, mask) -> None:
+    if face_average is not None:
+        face_average(vec, fields)   # opdssum + opcolv(vmult)   (utils.f90:339-340; add_noise_scal :284-285)
+        face_average(vec, fields)   # dsavg                      (:342-344; :286)
+    if mask is not None:            # bcdirVC / bcdirSC          (:347; :287)
+        ctx.call("nkv_op_diag", mask.ptr, vec.ptr, vec.ptr, 1.0, ctx.stream)
+
+
+def op_add_noise(ctx: NekContext, vec: NekVector, coords: dict, face_average=None, mask: NekVector | None = None):
+    """vx, vy[, vz] += op_add_noise's hash noise (utils.f90:297-359)."""
+    lay = ctx.layout
+    for c in range(lay.ldim):
+        mth_rand_add(ctx, vec, c, coords, NOISE_FC[c])
+    _finish(ctx, vec, range(lay.ldim), face_average, mask)
+
+
+def add_noise_scal(ctx: NekContext, vec: NekVector, field: int, coords: dict, fc, face_average=None,
+                   mask: NekVector | None = None):
+    """One scalar field += add_noise_scal's hash noise (utils.f90:258-295)."""
+    mth_rand_add(ctx, vec, field, coords, fc)
+    _finish(ctx, vec, (field,), face_average, mask)
+
+
+def noise_seed(ctx: NekContext, coords: dict, ifto: bool | None = None, ifpsco=(), face_average=None,
+               mask: NekVector | None = None) -> NekVector:
+    """The noise branch of ``prepare_seed`` (linear_stab.f90:254-265): zero, op_add_noise on the
+    velocity, add_noise_scal on t(:,1) if ``ifto`` (default: the layout has a scalar), and for every
+    passive scalar m = 2..ldimt with ``ifpsco(m-1)`` another add_noise_scal with (90 m, 300 m, 40 m)
+    — into t(:,1) again, as the reference writes it (:262).  Not normalised: pass the result to
+    ``krylov_schur.prepare_seed`` / ``seed_mode="normalize"`` (:287-291), or as the ``"noise"``
+    seed of the in-tree solver (eigensolvers.f90:192-203: k_normalize, one matvec)."""
+    lay = ctx.layout
+    if ifto is None:
+        ifto = lay.n_scalars > 0
+    if (ifto or any(ifpsco)) and lay.n_scalars == 0:
+        raise ValueError("ifto / ifpsco need a scalar field in the layout")
+    seed = ctx.vector()
+    seed.zero()
+    op_add_noise(ctx, seed, coords, face_average, mask)
+    t1 = lay.ldim
+    if ifto:
+        add_noise_scal(ctx, seed, t1, coords, SCAL_FC, face_average, mask)
+    for m, on in enumerate(ifpsco, start=2):
+        if on:
+            add_noise_scal(ctx, seed, t1, coords, (9.0e1 * m, 3.0e2 * m, 4.0e1 * m), face_average, mask)
+    return seed

@@ -10,7 +10,8 @@ What it restates (each function cites the reference line it follows):
   ``nekstab_oracle.c`` (reference operation order, no FP contraction);
 * the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
   ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, the legacy ``matvec`` dispatcher,
-  ``ts_steady_force_sensitivity``, ``newton_krylov``: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
+  ``ts_steady_force_sensitivity``, ``newton_krylov``, the seed noise ``mth_rand`` with its
+  direct-stiffness averaging: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
   dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
 
 Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
@@ -558,6 +559,77 @@ def wave_maker(L: OLayout, w, dRe, dIm, aRe, aIm):
     bi-orthogonalised vectors)."""
     vecs = biorthogonalize(L, w, dRe, dIm, aRe, aIm)
     return wavemaker_pointwise(L, *vecs), vecs
+
+
+def _cr(fn):
+    """fn rounded correctly to double (mpmath at 160 bits, then round-to-nearest)."""
+    import mpmath
+
+    def f(x):
+        with mpmath.workprec(160):
+            return float(fn(mpmath.mpf(x)))
+    return f
+
+
+def libm(kind="glibc"):
+    """(sin, cos): the host's glibc (gfortran's libm, as the reference links it) or correctly rounded."""
+    import math
+
+    if kind == "glibc":
+        return math.sin, math.cos
+    import mpmath
+    return _cr(mpmath.sin), _cr(mpmath.cos)
+
+
+def mth_rand(ix, iy, iz, ieg, xl, fc, if3d, sin=None, cos=None):
+    """utils.f90:408-418, one point: left-to-right operand order as written (fc(2)*ix*iy =
+    (fc(2)*ix)*iy); sin/cos default to the host's glibc."""
+    import math
+
+    sin, cos = sin or math.sin, cos or math.cos
+    r = fc[0] * (ieg + xl[0] * sin(xl[1])) + fc[1] * ix * iy + fc[2] * ix
+    if if3d:
+        r = fc[0] * (ieg + xl[2] * sin(r)) + fc[1] * iz * ix + fc[2] * iz
+    return cos(1.0e3 * sin(1.0e3 * sin(r)))
+
+
+def noise_field(nx, ny, nz, e_first, x, y, z, fc, kind="glibc", points=None):
+    """The pointwise noise op_add_noise / add_noise_scal add to one field (utils.f90:274-283,
+    318-335): element-major points, il fastest, ieg = e_first + e + 1.  ``kind``: the libm (see
+    ``libm``); ``points``: evaluate only these indices (the rest NaN)."""
+    sin, cos = libm(kind)
+    n = x.size
+    out = np.full(n, np.nan)
+    ppe = nx * ny * nz
+    for p in (range(n) if points is None else points):
+        e, r = divmod(int(p), ppe)
+        il, jl, kl = r % nx + 1, (r // nx) % ny + 1, r // (nx * ny) + 1
+        xl = (x[p], y[p], z[p] if z is not None else 0.0)
+        out[p] = mth_rand(float(il), float(jl), float(kl), float(e_first + e + 1), xl, fc, z is not None, sin, cos)
+    return out
+
+
+def coincident_average(q, coords, rel_tol=1e-9):
+    """dssum followed by vmult on one rank (Nek5000 gs '+', then the inverse multiplicity): every
+    point gets the mean of the points with the same coordinates, summed in ascending point order
+    and scaled by 1/count.  Independent grouping (a dict on rounded coordinates)."""
+    xs = [np.asarray(coords[k]) for k in ("x", "y", "z") if k in coords]
+    ext = max(float(np.ptp(a)) for a in xs) or 1.0
+    groups = {}
+    for p in range(xs[0].size):
+        key = tuple(int(round(float(a[p]) / (rel_tol * ext))) for a in xs)
+        groups.setdefault(key, []).append(p)
+    out = q.copy()
+    for members in groups.values():
+        if len(members) < 2:
+            continue
+        s = 0.0
+        for i in members:
+            s = s + q[i]
+        v = s * (1.0 / len(members))
+        for i in members:
+            out[i] = v
+    return out
 
 
 def boostconv_core(state, rb, w, nv_total):

@@ -207,6 +207,27 @@ def gen_wavemaker():
                         inputs_checksum=np.array([_checksum(v) for v in vecs]))
 
 
+def gen_noise():
+    """The reference's default seed noise on the real cylinder mesh: the GLL coordinates of
+    BF_1cyl0.f00001 (X block, byte-offset parse) in global element order, and the oracle's
+    op_add_noise (vx, vy: mth_rand, utils.f90:297-359, then dssum/vmult and dsavg by coincident
+    points) as checksums and every 97th value."""
+    import oracle as orc
+
+    _, _, emap, fields = _parse_std(os.path.join(REF, FLD_FILES[0]))
+    order = np.argsort(emap)
+    x, y = fields["x"][order].ravel(), fields["y"][order].ravel()
+    np.savez_compressed(os.path.join(HERE, "cyl_mesh_xy.npz"), x=x, y=y)
+    coords = {"x": x, "y": y}
+    out = {}
+    for c, fc in enumerate(((3.0e4, -1.5e3, 0.5e5), (2.3e4, 2.3e3, -2.0e5))):
+        q = orc.noise_field(6, 6, 1, 0, x, y, None, fc)
+        q = orc.coincident_average(orc.coincident_average(q, coords), coords)
+        out[f"c{c}_checksum"] = _checksum(q)
+        out[f"c{c}_sample"] = q[::97]
+    np.savez(os.path.join(HERE, "noise_cyl.npz"), **out)
+
+
 def gen_ordering():
     import oracle as orc
 
@@ -252,9 +273,13 @@ if __name__ == "__main__":
     if "--only-wavemaker" in sys.argv:   # needs only the committed bf_1cyl0_seed.npz, not /root/reference
         gen_wavemaker()
         sys.exit(0)
+    if "--only-noise" in sys.argv:
+        gen_noise()
+        sys.exit(0)
     gen_fld()
     gen_ordering()
     gen_solvers()
     gen_wavemaker()
+    gen_noise()
     for n in sorted(os.listdir(HERE)):
         print(f"{os.path.getsize(os.path.join(HERE, n)):10d}  {n}")
