@@ -398,6 +398,12 @@ int nkv_mth_rand_add(const nkv_layout* L, int lx1, int ly1, int lz1, int64_t e_f
                      const double* ym, const double* zm, double fc1, double fc2, double fc3, double* q,
                      void* stream);
 int nkv_group_average(int64_t n_groups, const int64_t* start, const int64_t* members, double* q, void* stream);
+/* add_symmetric_seed's perturbation (utils.f90:361-406, 3-D): qx = cos(alpha z) sin(2 pi y),
+ * qz = -(2 pi)/alpha cos(alpha z) cos(2 pi y), qt = cos(alpha z) cos(2 pi y) on n_v points (qy is
+ * left alone, as the reference does); alpha = 2 pi / (zmax - zmin).  The amplitude scaling
+ * 1e-6 / (0.5 sum glsc3(q, bm1, q)) is the host's (two dots and a scal). */
+int nkv_symmetric_seed(const nkv_layout* L, const double* ym, const double* zm, double alpha, double* qx,
+                       double* qz, double* qt, void* stream);
 
 /* ---- ts_gmres host helper (a17, newton_krylov.f90:250-269) -------------------------------
  * The least-squares residual ||beta e_1 - H(1:k+2, 1:k+1) y|| after one more Hessenberg column, in

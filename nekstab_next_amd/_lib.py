@@ -110,6 +110,7 @@ _SIGNATURES = {
     "nkv_fill_hash": (c_int, [_L, _P, c_uint64, c_int64, c_int64, _P]),
     "nkv_mth_rand_add": (c_int, [_L, c_int, c_int, c_int, c_int64, _P, _P, _P, c_double, c_double, c_double, _P, _P]),
     "nkv_group_average": (c_int, [c_int64, _P, _P, _P, _P]),
+    "nkv_symmetric_seed": (c_int, [_L, _P, _P, c_double, _P, _P, _P, _P]),
     "nkv_wavemaker": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
     "nkv_givens_column": (c_double, [c_int, _P, _P, _P, _P]),
     "nkv_gkl_coef": (c_int, [c_int, c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P]),

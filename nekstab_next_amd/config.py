@@ -16,8 +16,9 @@ class KrylovSchurConfig:
     #                           | "mgs2-icwy" (MGS in inverse compact WY form, 3 reads);
     #                           "dcgs2-native" | "cgs2-native" | "mgs2-native": the same sequences driven
     #                           by the library's one-call entry points (bit-identical)
-    seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" | "load" (a
-    #                                krylov_schur.load_seed vector; both eigensolvers.f90:192-223) | "as_is"
+    seed_mode: str = "normalize"   # "normalize" (linear_stab.f90:287-291) | "noise" (seeds.noise_seed) | "load"
+    #                                (a krylov_schur.load_seed vector; both eigensolvers.f90:192-223) |
+    #                                "symm" (seeds.symmetric_seed as Q(1), :205-208) | "as_is"
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
     graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)

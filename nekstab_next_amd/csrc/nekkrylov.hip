@@ -3175,6 +3175,38 @@ __global__ __launch_bounds__(kThreads) void k_group_average(int64_t n_groups, co
     }
 }
 
+// add_symmetric_seed's perturbation (utils.f90:361-406, before its amplitude scaling), pointwise:
+//   qx = cos(alpha z) sin(2 pi y),  qz = -(2 pi)/alpha cos(alpha z) cos(2 pi y),  qt = cos(alpha z) cos(2 pi y)
+// (qy is not written: the reference leaves it as it was).  No contraction, the reference's order.
+__global__ __launch_bounds__(kThreads) void k_symmetric_seed(int64_t n, const double* __restrict__ ym,
+                                                             const double* __restrict__ zm, double alpha,
+                                                             double* __restrict__ qx, double* __restrict__ qz,
+                                                             double* __restrict__ qt) {
+#pragma clang fp contract(off)
+    const double twopi = 2.0 * 3.14159265358979323846;
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kThreads) {
+        const double y = ym[p], z = zm[p];
+        qx[p] = cos(alpha * z) * sin(twopi * y);
+        qz[p] = -twopi / alpha * cos(alpha * z) * cos(twopi * y);
+        qt[p] = cos(alpha * z) * cos(twopi * y);
+    }
+}
+
+int nkv_symmetric_seed(const nkv_layout* L, const double* ym, const double* zm, double alpha, double* qx,
+                       double* qz, double* qt, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(ym, "ym"));
+    CHECK(check_ptr(zm, "zm"));
+    CHECK(check_ptr(qx, "qx"));
+    CHECK(check_ptr(qz, "qz"));
+    CHECK(check_ptr(qt, "qt"));
+    if (!(alpha != 0.0) || !std::isfinite(alpha)) return fail(NKV_EINVAL, "symmetric seed: alpha=%g", alpha);
+    hipLaunchKernelGGL(k_symmetric_seed, dim3(grid_for(L->n_v)), dim3(kThreads), 0, S(stream), L->n_v, ym, zm, alpha,
+                       qx, qz, qt);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
 int nkv_mth_rand_add(const nkv_layout* L, int lx1, int ly1, int lz1, int64_t e_first, const double* xm,
                      const double* ym, const double* zm, double fc1, double fc2, double fc3, double* q,
                      void* stream) {

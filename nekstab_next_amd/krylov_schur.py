@@ -172,7 +172,9 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
         from .vector import k_normalize
         k_normalize(w2)
         (op.rmatvec if transpose else op.matvec)(w2, Q[0])
-    elif cfg.seed_mode == "as_is":
+    elif cfg.seed_mode in ("as_is", "symm"):
+        # "symm": ifseed_symm (eigensolvers.f90:205-208): Q(1) = the symmetric seed as it stands
+        # (seeds.symmetric_seed), neither normalised nor mapped
         Q[0].copy_from(seed)
     else:
         raise ValueError(cfg.seed_mode)
@@ -199,7 +201,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # Gram–Schmidt no longer agree.  That mode therefore runs modified Gram–Schmidt: by default in
     # inverse compact WY form (the same coefficients, three reads of Q per step), or in the
     # reference's own operation order (cfg.nonorth_mode = "mgs2").
-    mode = _nonorth_of(cfg.mode, cfg) if (cfg.seed_mode in ("noise", "load") and start is None) else cfg.mode
+    mode = _nonorth_of(cfg.mode, cfg) if (cfg.seed_mode in ("noise", "load", "symm") and start is None) else cfg.mode
     if mode != cfg.mode:
         graphs, lazy = None, False
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)

@@ -173,3 +173,39 @@ def noise_seed(ctx: NekContext, coords: dict, ifto: bool | None = None, ifpsco=(
         if on:
             add_noise_scal(ctx, seed, t1, coords, (9.0e1 * m, 3.0e2 * m, 4.0e1 * m), face_average, mask)
     return seed
+
+
+def symmetric_seed(ctx: NekContext, coords: dict, base: NekVector | None = None) -> NekVector:
+    """``add_symmetric_seed(wrk%vx, wrk%vy, wrk%vz, wrk%t(:,1))`` (utils.f90:361-406, called at
+    eigensolvers.f90:205-208 when ``ifseed_symm``): on a copy of ``base`` (zero by default) vx, vz
+    and t(:,1) become cos(alpha z) sin(2 pi y), -(2 pi / alpha) cos(alpha z) cos(2 pi y) and
+    cos(alpha z) cos(2 pi y) with alpha = 2 pi / (zmax - zmin) over all ranks; vy keeps the base's
+    values (the reference never writes qy); then vx, vy, vz and t(:,1) are scaled by
+    1e-6 / (0.5 sum_c glsc3(q_c, bm1, q_c)) over the velocity components (bm1: the context's weights).
+    The in-tree solver takes the result as Q(1) unnormalised (``seed_mode="symm"``).  3-D with a
+    scalar field only (in 2-D the reference divides by zmax - zmin = 0)."""
+    lay = ctx.layout
+    if lay.ldim != 3 or lay.n_scalars < 1:
+        raise ValueError("add_symmetric_seed needs a 3-D layout with a scalar field (qp = t(:,1))")
+    _, y, z = _coord_tensors(ctx, coords)
+    zl = np.asarray(coords["z"], dtype=np.float64)
+    zmin = ctx.comm.min_scalar(float(zl.min()) if zl.size else np.inf, device=ctx.device)
+    zmax = ctx.comm.max_scalar(float(zl.max()) if zl.size else -np.inf, device=ctx.device)
+    alpha = 2.0 * np.pi / (zmax - zmin)
+    seed = ctx.vector()
+    if base is None:
+        seed.zero()
+    else:
+        seed.copy_from(base)
+    sv = lay.sv
+    ctx.call("nkv_symmetric_seed", y.data_ptr(), z.data_ptr(), float(alpha), seed.ptr, seed.ptr + 8 * 2 * sv,
+             seed.ptr + 8 * 3 * sv, ctx.stream)
+    vel = ctx.vector()
+    vel.copy_from(seed)
+    vel.storage[3 * sv:lay.n_wf * sv].zero_()       # amp over vx, vy, vz only (glsc3 x 3, :394-396)
+    amp = ctx.dot(vel, vel, time=False)
+    amp = 1e-6 / (0.50 * amp)
+    for c in (0, 1, 2, 3):                          # opcmult(qx, qy, qz, amp); cmult(qp, amp)
+        seg = seed.storage[c * sv:(c + 1) * sv]
+        seg.mul_(amp)
+    return seed

@@ -609,6 +609,25 @@ def noise_field(nx, ny, nz, e_first, x, y, z, fc, kind="glibc", points=None):
     return out
 
 
+def add_symmetric_seed(y, z, qy, w, zmin, zmax):
+    """utils.f90:361-406 on one rank's points (3-D): the spanwise-periodic perturbation, qy as given,
+    scaled by 1e-6 / (0.5 (glsc3(qx,bm1,qx) + glsc3(qy,bm1,qy) + glsc3(qz,bm1,qz))).  Returns
+    (qx, qy, qz, qp) — qp is the t(:,1) the in-tree solver passes (eigensolvers.f90:207)."""
+    pi = 4.0 * np.arctan(1.0)
+    alpha = 2 * pi / (zmax - zmin)
+    qx = np.cos(alpha * z) * np.sin(2.0 * pi * y)
+    qz = -(2.0 * pi) / alpha * np.cos(alpha * z) * np.cos(2.0 * pi * y)
+    qp = np.cos(alpha * z) * np.cos(2.0 * pi * y)
+    amp = glsc3_np(qx, w, qx) + glsc3_np(qy, w, qy) + glsc3_np(qz, w, qz)
+    amp = 1e-6 / (0.50 * amp)
+    return qx * amp, qy * amp, qz * amp, qp * amp
+
+
+def glsc3_np(a, w, b):
+    """Nek5000 glsc3 on one rank: sum of a*w*b in point order."""
+    return float(np.sum(a * w * b))
+
+
 def coincident_average(q, coords, rel_tol=1e-9):
     """dssum followed by vmult on one rank (Nek5000 gs '+', then the inverse multiplicity): every
     point gets the mean of the points with the same coordinates, summed in ascending point order

@@ -159,3 +159,48 @@ def test_seed_entry_checks(gpu):
         ctx.call_nl("nkv_group_average", 3, None, None, v.ptr, st)
     with pytest.raises(ValueError):
         seeds.mth_rand_add(ctx, v, lay.n_wf, co, seeds.SCAL_FC)
+
+
+def test_symmetric_seed_vs_oracle(gpu):
+    """add_symmetric_seed (utils.f90:361-406) as the in-tree solver calls it (eigensolvers.f90:
+    205-208: wrk%vx, wrk%vy, wrk%vz, wrk%t(:,1)): vy kept from the base vector, the amplitude from the
+    velocity dots with the weights; against the oracle (1e-13 relative: smooth functions, the
+    device's own sin/cos); then Krylov–Schur from it unnormalised (seed_mode "symm", MGS on the
+    non-orthonormal basis) against the oracle's run from the same Q(1)."""
+    import ctypes
+
+    from helpers import olayout, oracle_diag_matvec
+
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.krylov_schur import krylov_schur
+    from nekstab_next_amd.operators import DiagOperator
+
+    lay, co = _cases()["box3d"]
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=24)
+    base = ctx.vector()
+    base.fill_hash(9)
+    seed = seeds.symmetric_seed(ctx, co, base)
+    got = seed.to_packed()
+    qy = base.to_packed()[lay.sv: lay.sv + lay.n_v]
+    ref = orc.add_symmetric_seed(co["y"], co["z"], qy, w, co["z"].min(), co["z"].max())
+    for c, r in zip((0, 1, 2, 3), ref):
+        g = got[c * lay.sv: c * lay.sv + lay.n_v]
+        np.testing.assert_allclose(g, r, rtol=0, atol=1e-13 * np.max(np.abs(r)))
+    b = base.to_packed()
+    np.testing.assert_array_equal(got[4 * lay.sv:], b[4 * lay.sv:])   # pressure and time untouched
+    # Krylov-Schur from the unnormalised seed
+    L = olayout(lay)
+    d, _ = syn.diag_spectrum(lay)
+    dref = syn.to_reference_order(lay, d)
+    q1 = syn.to_reference_order(lay, got)
+    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="symm")
+    res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)
+    r = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
+    assert res.schur_cnt == r["schur_cnt"] and res.mstart_history == r["mstart"]
+    sel = np.abs(r["residual"]) < cfg.eigen_tol
+    for v in r["vals"][sel]:
+        assert np.min(np.abs(res.vals - v)) <= 1e-10 * abs(v)
+    with pytest.raises(ValueError):
+        seeds.symmetric_seed(NekContext(cylinder_layout(20), max_cols=4), {"x": np.zeros(720), "y": np.zeros(720)})
