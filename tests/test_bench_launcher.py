@@ -18,6 +18,13 @@ def _env(**kw):
     return env
 
 
+def _port(k: int) -> str:
+    """A rendezvous port per test and xdist worker, below the ephemeral range: a port picked free by
+    binding and releasing can be taken by a concurrently running test before the ranks bind it."""
+    w = os.environ.get("PYTEST_XDIST_WORKER", "gw0")
+    return str(21000 + 40 * int(w[2:] or 0) + k)
+
+
 def _run(args, env, timeout=120):
     return subprocess.run([sys.executable, BENCH, *args], env=env, capture_output=True, text=True, timeout=timeout)
 
@@ -75,7 +82,7 @@ def test_single_gpu_default_runs_in_process():
 # ---- round 3: bounded collectives, wall clocks, per-rank device identity ----
 
 def test_collective_probe_gathers_devices():
-    p = _run(["--gpus", "2", "--collective-probe"], _env(NKV_BACKEND="gloo"), timeout=120)
+    p = _run(["--gpus", "2", "--collective-probe"], _env(NKV_BACKEND="gloo", MASTER_PORT=_port(1)), timeout=120)
     assert p.returncode == 0, p.stderr
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert rec["world"] == 2 and rec["backend"] == "gloo" and rec["sum"] == 3.0
@@ -87,13 +94,15 @@ def test_collective_probe_gathers_devices():
 def test_rank_missing_from_allreduce_ends_every_rank():
     """One rank never joins the all-reduce: its peer's collective times out (bounded by
     NKV_COLLECTIVE_TIMEOUT_S instead of torch's 10 min), that rank exits non-zero, and the
-    launcher ends the absent rank and exits non-zero — all within the bound."""
+    launcher ends the absent rank and exits non-zero — all within the bound.  The bound also covers
+    the rendezvous (init_process_group), so it must exceed a loaded host's `import torch` in the
+    late rank (a 4 s bound failed the rendezvous under pytest -n 4)."""
     t0 = time.monotonic()
     p = _run(["--gpus", "2", "--collective-probe"],
-             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="4",
-                  NKV_LAUNCH_GRACE_S="2", NKV_RANK_WALL_S="0"), timeout=120)
+             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="20", MASTER_PORT=_port(2),
+                  NKV_LAUNCH_GRACE_S="2", NKV_RANK_WALL_S="0"), timeout=150)
     dt = time.monotonic() - t0
-    assert dt < 60, dt
+    assert dt < 90, dt
     assert p.returncode != 0
     assert "probe rank 0: all-reduce failed" in p.stderr, p.stderr[-2000:]
     assert "bench launcher: rank 0 exited with 3" in p.stderr
@@ -104,7 +113,7 @@ def test_rank_watchdog_ends_a_hung_rank():
     that never returns, with status 124 and a stack dump."""
     t0 = time.monotonic()
     p = _run(["--gpus", "2", "--collective-probe"],
-             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="600",
+             _env(NKV_BACKEND="gloo", NKV_PROBE_HANG_RANK="1", NKV_COLLECTIVE_TIMEOUT_S="600", MASTER_PORT=_port(3),
                   NKV_LAUNCH_GRACE_S="600", NKV_RANK_WALL_S="6", NKV_LAUNCH_WALL_S="0"), timeout=120)
     assert time.monotonic() - t0 < 60
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
