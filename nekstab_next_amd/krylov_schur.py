@@ -200,8 +200,9 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # unnormalised vector removes only part of the component) and classical and modified
     # Gram–Schmidt no longer agree.  That mode therefore runs modified Gram–Schmidt: by default in
     # inverse compact WY form (the same coefficients, three reads of Q per step), or in the
-    # reference's own operation order (cfg.nonorth_mode = "mgs2").
-    mode = _nonorth_of(cfg.mode, cfg) if (cfg.seed_mode in ("noise", "load", "symm") and start is None) else cfg.mode
+    # reference's own operation order (cfg.nonorth_mode = "mgs2").  A resumed run (``start``) keeps
+    # it too: its checkpointed basis descends from the same Q(1) (pass the original seed_mode).
+    mode = _nonorth_of(cfg.mode, cfg) if cfg.seed_mode in ("noise", "load", "symm") else cfg.mode
     if mode != cfg.mode:
         graphs, lazy = None, False
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)

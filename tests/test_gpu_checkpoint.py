@@ -42,6 +42,34 @@ def test_restart_from_checkpoint_matches_uninterrupted(gpu, tmp_path):
     np.testing.assert_allclose(np.sort(res.vals[conv].real)[::-1], exact, atol=1e-9)
 
 
+def test_noise_seeded_restart_keeps_mgs(gpu, tmp_path):
+    """The reference's default noise seed leaves Q(1) unnormalised, so the whole solve is modified
+    Gram–Schmidt ("mgs2-icwy"); a run resumed from its checkpoint (uparam(2) > 0, the same
+    seed_mode) must stay MGS too — a classical resume would change the factorisation — and
+    reproduces the uninterrupted run."""
+    lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
+    ctx = NekContext(lay, weights=syn.mass_weights(lay), max_cols=32)
+    d, exact = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d)
+    seed = ctx.vector()
+    seed.fill_hash(11)
+    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise")
+    ref = krylov_schur(ctx, op, seed, cfg)
+    hook = ArnoldiCheckpoint(ctx, str(tmp_path), session="cyl", evop="d")
+    krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=0, seed_mode="noise"), on_step=hook)
+    mstart = 9
+    Q, H = load_restart(ctx, str(tmp_path), "cyl", mstart, 16)
+    res = krylov_schur(ctx, op, None, cfg, Q=Q, start=(mstart, H))
+    assert res.schur_cnt == ref.schur_cnt >= 1 and res.mstart_history == ref.mstart_history
+    conv = ref.residual < 1e-6
+    np.testing.assert_allclose(res.vals[conv], ref.vals[conv], rtol=1e-11)
+    classical = krylov_schur(ctx, op, None, KrylovSchurConfig(k_dim=16, schur_tgt=0),
+                             Q=load_restart(ctx, str(tmp_path), "cyl", mstart, 16)[0], start=(mstart, H))
+    mgs = krylov_schur(ctx, op, None, KrylovSchurConfig(k_dim=16, schur_tgt=0, seed_mode="noise"),
+                       Q=load_restart(ctx, str(tmp_path), "cyl", mstart, 16)[0], start=(mstart, H))
+    assert np.max(np.abs(classical.H - mgs.H)) > 1e-8 * np.max(np.abs(mgs.H))
+
+
 def test_outpost_ks_files(gpu, tmp_path):
     """End of the in-tree solver: orthonormality.dat, Spectre_H/NS(_conv) files and the Re/Im
     eigenmode field files (eigensolvers.f90:335-349, 472-640)."""
