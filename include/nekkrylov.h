@@ -79,6 +79,7 @@ extern "C" {
 #define NKV_X_IS_LAST 0x20u /* block_dot2: x is column j-1 of Q (its two dots come from registers)  */
 #define NKV_MGS2 0x40u      /* update_hessenberg / arnoldi_factorization: the reference's MGS2 order */
 #define NKV_CHECK_BREAKDOWN 0x80u /* one-call factorisations: check the new H columns on return      */
+#define NKV_MGS_ICWY 0x100u /* arnoldi_factorization: both MGS passes in inverse compact WY form (3 reads) */
 
 typedef struct nkv_layout {
     int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */
@@ -310,7 +311,11 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
  * q_out = Q col mstep, hcol = H col mstep-1).  Same arguments as nkv_arnoldi_dcgs2; every column is
  * final when its step ends and columns < mstart are never written.  flags: NKV_TIME_DOT,
  * NKV_MGS2 (the reference's operation order, its dots all-reduced one at a time through the
- * callback: the sharded form of nkv_mgs2_step), NKV_CHECK_BREAKDOWN.
+ * callback: the sharded form of nkv_mgs2_step), NKV_MGS_ICWY (the same two MGS passes in inverse
+ * compact WY form, three reads of Q per step — see nkv_mgs_icwy_solve — for the non-orthonormal bases
+ * of the reference's default noise seed; the Gram rows of columns 1..mstart-2 are rebuilt first;
+ * scratch: nkv_arnoldi_scratch_doubles(mend), which covers its (mend+1)^2 Gram matrix),
+ * NKV_CHECK_BREAKDOWN.
  *
  * Breakdown (both one-call factorisations).  When the operator's Krylov space closes before mend
  * (A restricted to span(Q) is invariant: a rank-deficient operator), each later f is rounding noise.

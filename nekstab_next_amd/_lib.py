@@ -28,6 +28,7 @@ NKV_NORM2 = 0x8
 NKV_TIME_DOT = 0x10
 NKV_X_IS_LAST = 0x20
 NKV_MGS2 = 0x40
+NKV_MGS_ICWY = 0x100
 NKV_CHECK_BREAKDOWN = 0x80
 
 

@@ -40,6 +40,8 @@ Two orthogonalisation modes share the rest of the path:
   (the unnormalised noise/load seed, eigensolvers.f90:192-223; a restart with time in k_dot), where
   classical Gram–Schmidt gives a different factorisation.  Whole factorisations only
   (``arnoldi_factorization``): the Gram rows of the columns before ``mstart`` are rebuilt first.
+  ``"mgs2-icwy-native"``: the same sequence inside the library (``nkv_arnoldi_factorization`` with
+  ``NKV_MGS_ICWY``), bit-identical.
 
 No step synchronises the host: H lives on the device until the factorisation ends.
 """
@@ -460,6 +462,15 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         _dcgs2_close(ctx, Q, Hd, mend)
         on_step(mend)
         return
+    if mode == "mgs2-icwy-native":   # the "mgs2-icwy" sequence inside the library (one ABI call)
+        if on_step is None:
+            if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+                raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+            _settle_basis(Q, mstart, lazy=False)
+            _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
+                          flags=_lib.NKV_MGS_ICWY)
+            return
+        mode = "mgs2-icwy"
     if mode == "mgs2-icwy":
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")

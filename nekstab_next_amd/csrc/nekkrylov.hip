@@ -2397,7 +2397,12 @@ int nkv_dcgs2_update(const nkv_layout* L, const double* w, const double* Q, int 
 // 2-99: the loop :68-96 with update_hessenberg_matrix replaced by the DCGS2 entry points above).  The
 // host-side orchestration of nekstab_next_amd/arnoldi.py (_dcgs2_step / _dcgs2_close) in C++, for hosts
 // without Python: the caller supplies the operator and the all-reduce as callbacks.
-size_t nkv_arnoldi_scratch_doubles(int m) { return (size_t)(2 * (m + 1) + 4 * m + 16); }
+// DCGS2 / GMRES: [hd 2(m+1) | coef 4m+16];  NKV_MGS_ICWY: [hd 2(m+1) | h1 m+1 | h2 m+1 | nrm, pad | G (m+1)^2]
+static size_t icwy_scratch_doubles(int m) { return (size_t)(4 * (m + 1) + 2) + (size_t)(m + 1) * (size_t)(m + 1); }
+size_t nkv_arnoldi_scratch_doubles(int m) {
+    const size_t base = (size_t)(2 * (m + 1) + 4 * m + 16), icwy = icwy_scratch_doubles(m);
+    return base > icwy ? base : icwy;
+}
 
 // NKV_CHECK_BREAKDOWN: after a one-call factorisation, synchronise and test the new H columns c0..c1-1
 // (include/nekkrylov.h, "Breakdown").  The same rule as nekstab_next_amd.krylov_schur.breakdown_column.
@@ -2616,6 +2621,43 @@ int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, i
     if (mstart < 1 || mend > NKV_MAX_COLS) return fail(NKV_EINVAL, "steps %d..%d outside 1..%d", mstart, mend, NKV_MAX_COLS);
     if (mend < mstart) return NKV_OK;
     if (ldh < mend + 1) return fail(NKV_EINVAL, "ldh=%lld < mend+1=%d", (long long)ldh, mend + 1);
+    if (flags & NKV_MGS_ICWY) {   // the "mgs2-icwy" sequence of nekstab_next_amd/arnoldi.py (_icwy_step)
+        if (flags & NKV_MGS2) return fail(NKV_EINVAL, "NKV_MGS2 and NKV_MGS_ICWY are exclusive");
+        CHECK(check_ptr(w, "w"));
+        CHECK(check_ptr(ws, "ws"));
+        const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+        const unsigned dotf = NKV_TIME | (tf ? NKV_TIME_DOT : 0u);
+        const int64_t ldg = mend + 1;
+        double* hd = scratch_dev;
+        double* h1 = hd + 2 * ldg;
+        double* h2 = h1 + ldg;
+        double* nrm = h2 + ldg;
+        double* G = nrm + 2;   // 16-byte aligned (the scratch is)
+        auto col = [L, Q](int c) { return Q + (int64_t)c * L->ld; };
+        auto reduce = [&](double* buf, int n, const char* what) -> int {
+            if (!allreduce) return NKV_OK;
+            const int rc = allreduce(ar_user, buf, n, stream);
+            return rc == 0 ? NKV_OK : fail(NKV_ECALLBACK, "allreduce callback returned %d (%s)", rc, what);
+        };
+        for (int i = 1; i + 1 < mstart; ++i) {   // Gram rows of the columns before mstart (row mstart-1: step mstart)
+            CHECK(nkv_block_dot(L, w, Q, i, col(i), G + i * ldg, ws, tf, stream));
+            CHECK(reduce(G + i * ldg, i, "Gram row"));
+        }
+        for (int j = mstart; j <= mend; ++j) {
+            const int rc = matvec(mv_user, col(j - 1), f, stream);
+            if (rc != 0) return fail(NKV_ECALLBACK, "matvec callback returned %d at step %d", rc, j);
+            CHECK(nkv_block_dot2(L, w, Q, j, col(j - 1), f, hd, ws, tf | NKV_X_IS_LAST, stream));
+            CHECK(reduce(hd, 2 * j, "Gram row and first MGS pass"));
+            CHECK(nkv_mgs_icwy_solve(j, G, ldg, hd, hd + j, h1, stream));
+            CHECK(nkv_block_update_dot(L, w, Q, j, h1, f, h2, ws, dotf, stream));
+            CHECK(reduce(h2, j, "second MGS pass"));
+            CHECK(nkv_mgs_icwy_solve(j, G, ldg, nullptr, h2, h2, stream));
+            CHECK(nkv_block_update(L, w, Q, j, h2, f, nrm, ws, NKV_NORM2 | dotf, stream));
+            CHECK(reduce(nrm, 1, "norm"));
+            CHECK(nkv_arnoldi_finish(L, f, nrm, col(j), j, h1, h2, H_dev + (int64_t)(j - 1) * ldh, 0, stream));
+        }
+        return (flags & NKV_CHECK_BREAKDOWN) ? check_breakdown(H_dev, ldh, mstart - 1, mend, ws, stream) : NKV_OK;
+    }
     const unsigned uf = flags & (NKV_TIME_DOT | NKV_MGS2);
     for (int j = mstart; j <= mend; ++j) {   // f = A Q(j); orthonormalise against Q(1..j); Q(j+1) = f (:75-81)
         double* x = Q + (int64_t)(j - 1) * L->ld;

@@ -64,7 +64,7 @@ def _nonorth_of(mode: str, cfg: KrylovSchurConfig) -> str:
         return _mgs2_of(mode)
     if cfg.nonorth_mode != "mgs2-icwy":
         raise ValueError(f"nonorth_mode={cfg.nonorth_mode!r}: 'mgs2-icwy' or 'mgs2'")
-    return cfg.nonorth_mode
+    return "mgs2-icwy-native" if mode.endswith("-native") else "mgs2-icwy"
 
 
 def breakdown_column(H: np.ndarray, c0: int, k: int, tol: float, offset: int = 1) -> int:

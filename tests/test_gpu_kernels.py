@@ -545,7 +545,8 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
 
 
 @pytest.mark.parametrize("time_dot", [True, False])
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "cgs2-native", "mgs2-native"])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "cgs2-native", "mgs2-native",
+                                  "mgs2-icwy-native"])
 def test_arnoldi_with_time_component_vs_oracle(gpu, mode, time_dot):
     """The scalar `time` follows every update and the operator propagates it (time_scale); with
     uparam(1)==2.1 it also enters k_dot (krylov_subspace.f90:52-54), otherwise it is carried but
@@ -608,7 +609,7 @@ def test_mgs2_icwy_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
     out = {}
     for name, mode, splits in (("one", "mgs2-icwy", [(1, m)]), ("split", "mgs2-icwy", [(1, 5), (6, m)]),
-                               ("cgs2", "cgs2", [(1, m)])):
+                               ("cgs2", "cgs2", [(1, m)]), ("native", "mgs2-icwy-native", [(1, 5), (6, m)])):
         Q = ctx.basis(m + 1)
         Q[0].from_packed(q0)
         Hd = HessenbergDev(ctx, m)
@@ -621,6 +622,9 @@ def test_mgs2_icwy_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     assert np.max(np.abs(H - Hr)) <= 1e-12 * hmax, np.max(np.abs(H - Hr)) / hmax
     np.testing.assert_allclose(Qg, Qr, rtol=0, atol=1e-11 * max(1.0, scale))
     assert np.max(np.abs(out["split"][0] - H)) <= 1e-13 * hmax
+    # the library's one-call sequence (nkv_arnoldi_factorization, NKV_MGS_ICWY) is the Python one
+    np.testing.assert_array_equal(out["native"][0], out["split"][0])
+    np.testing.assert_array_equal(out["native"][1], out["split"][1])
     if scale != 1.0:
         assert np.max(np.abs(out["cgs2"][0] - Hr)) > 1e-6 * hmax
 

@@ -421,9 +421,10 @@ def test_krylov_schur_knobs(gpu):
     q1 = np.zeros(L.len)
     orc.lib().orc_op_diag(ctypes.byref(L.c), dref, sn, q1, 0.0)
     ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
-    for nonorth in ("mgs2-icwy", "mgs2"):   # MGS in inverse compact WY form (default) / reference order
+    for nonorth, mode in (("mgs2-icwy", "dcgs2"), ("mgs2", "dcgs2"), ("mgs2-icwy", "dcgs2-native")):
+        # MGS in inverse compact WY form (default; in the library for a native mode) / reference order
         res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise",
-                                                            nonorth_mode=nonorth))
+                                                            nonorth_mode=nonorth, mode=mode))
         _compare_ks(res, ref, KrylovSchurConfig(k_dim=16, schur_tgt=5))
         assert res.schur_cnt >= 1 and not res.breakdowns
     # as_is: the caller's vector is the first basis vector
