@@ -380,12 +380,31 @@ def collective_probe() -> int:
     except Exception as e:  # noqa: BLE001 - the bounded collective's timeout, reported and fatal
         print(f"probe rank {comm.rank}: all-reduce failed after {time.monotonic() - t0:.1f} s: "
               f"{type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}", file=sys.stderr, flush=True)
-        return 3
+        sys.stdout.flush()
+        os._exit(3)   # no interpreter teardown under a broken group (c10d's threads can abort it: -6)
     if comm.rank == 0:
         print(json.dumps({"collective_probe": True, "world": comm.world, "backend": comm.backend,
                           "sum": float(t.item()), "devices": devs,
                           "distinct_devices": distinct_devices(devs)}), flush=True)
+    _leave_group(comm)
     return 0
+
+
+def _leave_group(comm) -> None:
+    """Every rank leaves the process group together, then the process ends without the
+    interpreter's teardown: c10d's background threads, torn down by static destructors at exit, were
+    seen to abort a gloo rank ("terminate called without an active exception", status -6) after its
+    work was done — which a launcher reports as a failed job."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    comm.barrier()
+    dist.destroy_process_group()
+    if comm.world > 1:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 def distinct_devices(devs) -> bool | None:
@@ -676,11 +695,8 @@ def run(args):
             "krylov_schur_leg": ks_leg,
         }
         print(json.dumps(out), file=args.json_out, flush=True)
-    comm.barrier()
-    import torch.distributed as dist
-
-    if dist.is_available() and dist.is_initialized():
-        dist.destroy_process_group()   # every rank leaves the RCCL group before the process exits
+    args.json_out.flush()
+    _leave_group(comm)   # every rank leaves the RCCL group before the process exits
 
 
 if __name__ == "__main__":
