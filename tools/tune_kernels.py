@@ -156,6 +156,11 @@ VARIANTS = {
     "d2cs4_b1024": {"patch": "d2_colsplit", "NKV_D2_CG": 4, "NKV_D2_CG_B": 1024},
     "d2cs2_j32": {"patch": "d2_colsplit", "NKV_D2_CG_J": 32},
     "d2cs2_b512_j32": {"patch": "d2_colsplit", "NKV_D2_CG_B": 512, "NKV_D2_CG_J": 32},
+    # ... or into sequential launches over column segments (half the basis pages open at a time)
+    "d2seq2": {"patch": "d2_seqsplit"},
+    "d2seq2_j48": {"patch": "d2_seqsplit", "NKV_D2_CG_J": 48},
+    "d2seq2_j96": {"patch": "d2_seqsplit", "NKV_D2_CG_J": 96},
+    "d2seq3": {"patch": "d2_seqsplit", "NKV_D2_CG": 3},
 }
 
 
