@@ -4,7 +4,8 @@
 ! Arnoldi relation A Q_m = Q_{m+1} H checked through the same calls; then ts_gmres
 ! (newton_krylov.f90:241-294) with its inner loop as ONE library call (nkv_gmres_dcgs2): restarts,
 ! the small least-squares problem on the host (Givens + back substitution here; the reference's
-! lstsq/dgels in nekStab), x += Q y with nkv_combine.   usage: arnoldi_f [E [m]]
+! lstsq/dgels in nekStab), x += Q y with nkv_combine; then an unnormalised Q(1) (the default noise
+! seed) through nkv_arnoldi_factorization with NKV_MGS2 and NKV_MGS_ICWY.   usage: arnoldi_f [E [m]]
 module diag_callback
    ! the operator handed to nkv_arnoldi_dcgs2 as a callback: y = d .* x on the library's stream
    use iso_c_binding
@@ -34,7 +35,7 @@ program arnoldi_f
    real(c_double), allocatable, target :: hw(:), H(:, :), g(:), dh(:)
    real(c_double), target :: r2
    real(c_double) :: orth, arn, hmax
-   logical :: gm_ok
+   logical :: gm_ok, mg_ok
 
    E = 512; m = 24
    nargs = command_argument_count()
@@ -143,13 +144,51 @@ program arnoldi_f
       print '(a)', 'arnoldi_f: nkv_arnoldi_dcgs2 DIFFERS from the step-by-step loop'
    end if
    call gmres_leg(gm_ok)
-   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12 .and. same .and. gm_ok) then
+   call mgs_leg(mg_ok)
+   if (orth < 1.0d-12 .and. arn/hmax < 1.0d-12 .and. same .and. gm_ok .and. mg_ok) then
       print '(a)', 'arnoldi_f: OK'
    else
       print '(a)', 'arnoldi_f: FAILED'
       stop 1
    end if
 contains
+
+   subroutine mgs_leg(ok)
+      ! the in-tree solver's default noise seed leaves Q(1) unnormalised (eigensolvers.f90:192-203):
+      ! only modified Gram-Schmidt reproduces the reference there.  nkv_arnoldi_factorization with
+      ! NKV_MGS2 (the reference's per-column order) and with NKV_MGS_ICWY (inverse compact WY form,
+      ! three reads of Q per step) must agree to rounding.
+      logical, intent(out) :: ok
+      type(c_ptr) :: Qa, Qb, Ha, Hb, sc
+      real(c_double), allocatable, target :: Hah(:, :), Hbh(:, :)
+      real(c_double) :: dmax
+      integer :: mm
+      mm = min(m, 16)
+      call ck(hipMalloc(Qa, (mm + 1)*vbytes), 'hipMalloc Qa')
+      call ck(hipMalloc(Qb, (mm + 1)*vbytes), 'hipMalloc Qb')
+      call ck(hipMalloc(Ha, int(mm*(mm + 1), c_size_t)*8), 'hipMalloc Ha')
+      call ck(hipMalloc(Hb, int(mm*(mm + 1), c_size_t)*8), 'hipMalloc Hb')
+      call ck(hipMalloc(sc, nkv_arnoldi_scratch_doubles(int(mm, c_int))*8), 'hipMalloc scratch')
+      call ck(hipMemset(Ha, 0, int(mm*(mm + 1), c_size_t)*8), 'memset Ha')
+      call ck(hipMemset(Hb, 0, int(mm*(mm + 1), c_size_t)*8), 'memset Hb')
+      call ck(nkv_fill_hash(L, Qb, 7_c_int64_t, 0_c_int64_t, 0_c_int64_t, st), 'seed')
+      call ck(nkv_dot(L, w, Qb, Qb, nrm, ws, 0, st), 'seed norm')
+      call ck(nkv_normalize_dev(L, Qb, nrm, c_null_ptr, 0, st), 'normalise')
+      call ck(nkv_op_diag(L, d, Qb, Qa, 0.0d0, st), 'A seed')                  ! Q(1) = A s/||s||
+      call ck(nkv_op_diag(L, d, Qb, Qb, 0.0d0, st), 'A seed (in place)')
+      call ck(nkv_arnoldi_factorization(L, w, Qa, 1, int(mm, c_int), Ha, int(mm + 1, c_int64_t), f, sc, ws, &
+                                        c_funloc(diag_mv), c_null_ptr, c_null_funptr, c_null_ptr, NKV_MGS2, st), 'mgs2')
+      call ck(nkv_arnoldi_factorization(L, w, Qb, 1, int(mm, c_int), Hb, int(mm + 1, c_int64_t), f, sc, ws, &
+                                        c_funloc(diag_mv), c_null_ptr, c_null_funptr, c_null_ptr, NKV_MGS_ICWY, st), 'icwy')
+      call ck(nkv_check_status(ws, st), 'NaN check')
+      allocate (Hah(mm + 1, mm), Hbh(mm + 1, mm))
+      call ck(hipMemcpy(c_loc(Hah), Ha, int(mm*(mm + 1), c_size_t)*8, hipMemcpyDeviceToHost), 'Ha down')
+      call ck(hipMemcpy(c_loc(Hbh), Hb, int(mm*(mm + 1), c_size_t)*8, hipMemcpyDeviceToHost), 'Hb down')
+      dmax = maxval(abs(Hah - Hbh))/maxval(abs(Hah))
+      print '(a,i0,a,es10.3)', 'arnoldi_f: unnormalised Q(1), ', mm, &
+         ' MGS2 steps: max|H(NKV_MGS_ICWY) - H(NKV_MGS2)|/max|H| = ', dmax
+      ok = dmax < 1.0d-12
+   end subroutine mgs_leg
 
    subroutine gmres_leg(ok)
       ! ts_gmres: Q(:,1) = r/||r||; inner loop = nkv_gmres_dcgs2; y = argmin ||beta e1 - H y||;

@@ -1002,7 +1002,9 @@ def test_c_host_example_runs(gpu):
 
 def test_fortran_host_example_runs(gpu):
     """examples/fortran_host/arnoldi_f: the DCGS2 loop of INTEGRATION.md §2b from Fortran through the
-    bind(C) interface (the reference's language): W-orthonormality and Arnoldi relation to 1e-12."""
+    bind(C) interface (the reference's language): W-orthonormality and Arnoldi relation to 1e-12;
+    and the default noise seed's unnormalised Q(1) through nkv_arnoldi_factorization with NKV_MGS2 and
+    with NKV_MGS_ICWY, equal to 1e-12 of max|H|."""
     import os
     import subprocess
 
@@ -1013,6 +1015,7 @@ def test_fortran_host_example_runs(gpu):
     p = subprocess.run([exe, "512", "24"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "arnoldi_f: OK" in p.stdout
+    assert "unnormalised Q(1)" in p.stdout
 
 
 @pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "dcgs2-lazy"])
