@@ -1941,6 +1941,173 @@ int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q,
 // ==========================================================================================
 // C ABI
 // ==========================================================================================
+// ---- bf_sensitivity (sensitivity.f90:81-269): gradm1 and the pointwise sensitivity terms -------------
+//
+// gradm1 (Nek5000 navier5.f; not in the reference tree) with the geometric factors of Nek5000's
+// glmapm1 / xyzrst (coef.f) computed on the fly from the GLL coordinates: for every point
+//   xr = sum_m D(i,m) x(m,j,k),  xs = sum_m D(j,m) x(i,m,k),  xt = sum_m D(k,m) x(i,j,m)   (mxm order)
+//   2-D: jac = xr ys - xs yr;  rx = ys, ry = -xs, sx = -yr, sy = xr
+//   3-D: jac = xr ys zt + xt yr zs + xs yt zr - xr yt zs - xs yr zt - xt ys zr (addcol4 / subcol4),
+//        rx = ys zt - yt zs, ry = xt zs - xs zt, rz = xs yt - xt ys, sx = yt zr - yr zt, ...  (ascol5)
+//   ux = (1/jac) (ur rx + us sx [+ ut tx]),  uy, uz likewise
+// One workgroup holds `epb` whole elements in LDS (coordinates, u, D); each thread owns one point.
+// No contraction (the reference's operand order).  Element-local: it shards with the elements.
+template <int LDIM>
+__global__ __launch_bounds__(1024) void k_gradm1(int nx, int64_t nel, int epb, const double* __restrict__ Dg,
+                                                 const double* __restrict__ xm, const double* __restrict__ ym,
+                                                 const double* __restrict__ zm, const double* __restrict__ u,
+                                                 double* __restrict__ ux, double* __restrict__ uy,
+                                                 double* __restrict__ uz) {
+#pragma clang fp contract(off)
+    extern __shared__ double lds[];
+    const int pts = LDIM == 3 ? nx * nx * nx : nx * nx;
+    const int nt = epb * pts;
+    double* D = lds;
+    double* X = D + nx * nx;
+    double* Y = X + nt;
+    double* Z = Y + nt;              // 3-D only
+    double* U = LDIM == 3 ? Z + nt : Z;
+    for (int t = threadIdx.x; t < nx * nx; t += blockDim.x) D[t] = Dg[t];
+    const int tid = threadIdx.x;
+    const int le = tid / pts, r = tid - le * pts;
+    const int i = r % nx, j = (r / nx) % nx, k = LDIM == 3 ? r / (nx * nx) : 0;
+    const int base = le * pts;
+    for (int64_t e0 = (int64_t)blockIdx.x * epb; e0 < nel; e0 += (int64_t)gridDim.x * epb) {
+        const int64_t p = e0 * pts + tid;
+        const bool live = tid < nt && e0 + le < nel;
+        __syncthreads();   // the previous group's reads are done (and D is staged on the first pass)
+        if (live) {
+            X[tid] = xm[p];
+            Y[tid] = ym[p];
+            if (LDIM == 3) Z[tid] = zm[p];
+            U[tid] = u[p];
+        }
+        __syncthreads();
+        if (!live) continue;
+        const int sj = nx, sk = nx * nx;            // strides of s and t inside an element
+        const int ri = base + j * sj + k * sk;      // line along r through (., j, k)
+        const int si = base + i + k * sk;           // line along s through (i, ., k)
+        const int ti = base + i + j * sj;           // line along t through (i, j, .)
+        const double* Di = D + i * nx;
+        const double* Dj = D + j * nx;
+        double xr = Di[0] * X[ri], yr = Di[0] * Y[ri], ur = Di[0] * U[ri];
+        double xs = X[si] * Dj[0], ys = Y[si] * Dj[0], us = U[si] * Dj[0];
+        for (int m = 1; m < nx; ++m) {
+            xr = xr + Di[m] * X[ri + m];
+            yr = yr + Di[m] * Y[ri + m];
+            ur = ur + Di[m] * U[ri + m];
+            xs = xs + X[si + m * sj] * Dj[m];
+            ys = ys + Y[si + m * sj] * Dj[m];
+            us = us + U[si + m * sj] * Dj[m];
+        }
+        if constexpr (LDIM == 2) {
+            double jac = 0.0;
+            jac = jac + xr * ys;
+            jac = jac - xs * yr;
+            const double rx = ys, ry = -xs, sx = -yr, sy = xr;
+            const double jacmi = 1.0 / jac;
+            ux[p] = jacmi * (ur * rx + us * sx);
+            uy[p] = jacmi * (ur * ry + us * sy);
+        } else {
+            const double* Dk = D + k * nx;
+            double zr = Di[0] * Z[ri], zs = Z[si] * Dj[0];
+            double xt = X[ti] * Dk[0], yt = Y[ti] * Dk[0], zt = Z[ti] * Dk[0], ut = U[ti] * Dk[0];
+            for (int m = 1; m < nx; ++m) {
+                zr = zr + Di[m] * Z[ri + m];
+                zs = zs + Z[si + m * sj] * Dj[m];
+                xt = xt + X[ti + m * sk] * Dk[m];
+                yt = yt + Y[ti + m * sk] * Dk[m];
+                zt = zt + Z[ti + m * sk] * Dk[m];
+                ut = ut + U[ti + m * sk] * Dk[m];
+            }
+            double jac = 0.0;
+            jac = jac + xr * ys * zt;
+            jac = jac + xt * yr * zs;
+            jac = jac + xs * yt * zr;
+            jac = jac - xr * yt * zs;
+            jac = jac - xs * yr * zt;
+            jac = jac - xt * ys * zr;
+            const double rx = ys * zt - yt * zs, ry = xt * zs - xs * zt, rz = xs * yt - xt * ys;
+            const double sx = yt * zr - yr * zt, sy = xr * zt - xt * zr, sz = xt * yr - xr * yt;
+            const double tx = yr * zs - ys * zr, ty = xs * zr - xr * zs, tz = xr * ys - xs * yr;
+            const double jacmi = 1.0 / jac;
+            ux[p] = jacmi * (ur * rx + us * sx + ut * tx);
+            uy[p] = jacmi * (ur * ry + us * sy + ut * ty);
+            uz[p] = jacmi * (ur * rz + us * sz + ut * tz);
+        }
+    }
+}
+
+// The pointwise part of bf_sensitivity (sensitivity.f90:202-235, 258-259) after gradm1 + dsavg:
+// tr, ti (direct-gradient terms), pr, pi (adjoint-gradient terms), then sr = tr + pr, si = ti + pi,
+// each accumulated from zero in the reference's opaddcol3 order (a += b c, no contraction).  The
+// reference's index slips are kept: its lines 204/207/213/216 multiply vy_a* by dwdz_d* (not dvdz_d*)
+// in the z component.  In 2-D the reference's vz terms read arrays it never set (opcopy skips vz);
+// here they are absent.  G: gradients [mode dRe,dIm,aRe,aIm][component u,v,w][direction x,y,z], each a
+// field segment of sv doubles; out: [tr, ti, pr, pi, sr, si][component], segments of sv doubles.
+template <int LDIM>
+__global__ __launch_bounds__(kThreads) void k_bf_sensitivity(int64_t n, int64_t sv, const double* __restrict__ dRe,
+                                                             const double* __restrict__ dIm,
+                                                             const double* __restrict__ aRe,
+                                                             const double* __restrict__ aIm,
+                                                             const double* __restrict__ G, double* __restrict__ out) {
+#pragma clang fp contract(off)
+    enum { DR = 0, DI = 1, AR = 2, AI = 3 };
+    for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kThreads) {
+        // gradient d(comp)/d(dir) of mode md at this point; components/directions beyond 2-D read nothing
+        auto g = [&](int md, int c, int d) -> double {
+            return (c < LDIM && d < LDIM) ? G[((int64_t)(md * LDIM + c) * LDIM + d) * sv + p] : 0.0;
+        };
+        double v[4][3];
+        const double* modes[4] = {dRe, dIm, aRe, aIm};
+#pragma unroll
+        for (int md = 0; md < 4; ++md)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) v[md][c] = c < LDIM ? modes[md][c * sv + p] : 0.0;
+        double tr[3] = {0.0, 0.0, 0.0}, ti[3] = {0.0, 0.0, 0.0}, pr[3] = {0.0, 0.0, 0.0}, pi[3] = {0.0, 0.0, 0.0};
+        // opaddcol3(a1, a2, a3, b, b, b, c1, c2, c3): a_c = a_c + b c_c (a3 only in 3-D)
+        auto add = [&](double* a, double b, double c1, double c2, double c3) {
+            a[0] = a[0] + b * c1;
+            a[1] = a[1] + b * c2;
+            if (LDIM == 3) a[2] = a[2] + b * c3;
+        };
+        const int X = 0, Y = 1, Z = 2, U = 0, V = 1, W = 2;
+        add(tr, -v[AR][U], g(DR, U, X), g(DR, U, Y), g(DR, U, Z));                    // :203
+        add(tr, -v[AR][V], g(DR, V, X), g(DR, V, Y), g(DR, W, Z));                    // :204 (dwdz)
+        if (LDIM == 3) add(tr, -v[AR][W], g(DR, W, X), g(DR, W, Y), g(DR, W, Z));     // :205
+        add(tr, -v[AI][U], g(DI, U, X), g(DI, U, Y), g(DI, U, Z));                    // :206
+        add(tr, -v[AI][V], g(DI, V, X), g(DI, V, Y), g(DI, W, Z));                    // :207 (dwdz)
+        if (LDIM == 3) add(tr, -v[AI][W], g(DI, W, X), g(DI, W, Y), g(DI, W, Z));     // :208
+        add(ti, v[AR][U], g(DI, U, X), g(DI, U, Y), g(DI, U, Z));                     // :212
+        add(ti, v[AR][V], g(DI, V, X), g(DI, V, Y), g(DI, W, Z));                     // :213 (dwdz)
+        if (LDIM == 3) add(ti, v[AR][W], g(DI, W, X), g(DI, W, Y), g(DI, W, Z));      // :214
+        add(ti, -v[AI][U], g(DR, U, X), g(DR, U, Y), g(DR, U, Z));                    // :215
+        add(ti, -v[AI][V], g(DR, V, X), g(DR, V, Y), g(DR, W, Z));                    // :216 (dwdz)
+        if (LDIM == 3) add(ti, -v[AI][W], g(DR, W, X), g(DR, W, Y), g(DR, W, Z));     // :217
+        add(pr, v[DR][U], g(AR, U, X), g(AR, V, X), g(AR, W, X));                     // :221
+        add(pr, v[DR][V], g(AR, U, Y), g(AR, V, Y), g(AR, W, Y));                     // :222
+        if (LDIM == 3) add(pr, v[DR][W], g(AR, U, Z), g(AR, V, Z), g(AR, W, Z));      // :223
+        add(pr, v[DI][U], g(AI, U, X), g(AI, V, X), g(AI, W, X));                     // :224
+        add(pr, v[DI][V], g(AI, U, Y), g(AI, V, Y), g(AI, W, Y));                     // :225
+        if (LDIM == 3) add(pr, v[DI][W], g(AI, U, Z), g(AI, V, Z), g(AI, W, Z));      // :226
+        add(pi, v[DR][U], g(AI, U, X), g(AI, V, X), g(AI, W, X));                     // :230
+        add(pi, v[DR][V], g(AI, U, Y), g(AI, V, Y), g(AI, W, Y));                     // :231
+        if (LDIM == 3) add(pi, v[DR][W], g(AI, U, Z), g(AI, V, Z), g(AI, W, Z));      // :232
+        add(pi, -v[DI][U], g(AR, U, X), g(AR, V, X), g(AR, W, X));                    // :233
+        add(pi, -v[DI][V], g(AR, U, Y), g(AR, V, Y), g(AR, W, Y));                    // :234
+        if (LDIM == 3) add(pi, -v[DI][W], g(AR, U, Z), g(AR, V, Z), g(AR, W, Z));     // :235
+#pragma unroll
+        for (int c = 0; c < LDIM; ++c) {
+            out[(0 * LDIM + c) * sv + p] = tr[c];
+            out[(1 * LDIM + c) * sv + p] = ti[c];
+            out[(2 * LDIM + c) * sv + p] = pr[c];
+            out[(3 * LDIM + c) * sv + p] = pi[c];
+            out[(4 * LDIM + c) * sv + p] = tr[c] + pr[c];   // opadd2, :258
+            out[(5 * LDIM + c) * sv + p] = ti[c] + pi[c];   // :259
+        }
+    }
+}
+
 extern "C" {
 
 int nkv_abi_version(void) { return NKV_ABI_VERSION; }
@@ -3290,6 +3457,58 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
     const int64_t pairs = L->sv / 2;
     auto kern = ncomp == 3 ? k_wavemaker<3> : k_wavemaker<2>;
     hipLaunchKernelGGL(kern, dim3(grid_for(pairs)), dim3(kThreads), 0, S(stream), dRe, dIm, aRe, aIm, out, L->sv, pairs);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const double* xm, const double* ym,
+               const double* zm, const double* u, double* ux, double* uy, double* uz, void* stream) {
+    CHECK(check_layout(L));
+    if (ldim != 2 && ldim != 3) return fail(NKV_EINVAL, "gradm1: ldim=%d must be 2 or 3", ldim);
+    if (lx1 < 2 || lx1 > 10) return fail(NKV_EINVAL, "gradm1: lx1=%d outside 2..10", lx1);
+    const int pts = ldim == 3 ? lx1 * lx1 * lx1 : lx1 * lx1;
+    if (L->n_v % pts != 0)
+        return fail(NKV_EINVAL, "gradm1: %d points per element do not divide n_v=%lld", pts, (long long)L->n_v);
+    if ((ldim == 3) != (zm != nullptr)) return fail(NKV_EINVAL, "gradm1: zm must be given exactly in 3-D");
+    if ((ldim == 3) != (uz != nullptr)) return fail(NKV_EINVAL, "gradm1: uz must be given exactly in 3-D");
+    CHECK(check_ptr(D, "D"));
+    CHECK(check_ptr(xm, "xm"));
+    CHECK(check_ptr(ym, "ym"));
+    CHECK(check_ptr(u, "u"));
+    CHECK(check_ptr(ux, "ux"));
+    CHECK(check_ptr(uy, "uy"));
+    const int64_t nel = L->n_v / pts;
+    if (nel == 0) return NKV_OK;
+    const int epb = pts >= 256 ? 1 : 256 / pts;            // whole elements per workgroup
+    const int threads = ((epb * pts + 63) / 64) * 64;       // whole waves
+    const size_t lds = sizeof(double) * ((size_t)lx1 * lx1 + (size_t)(ldim + 1) * epb * pts);
+    const int64_t groups = (nel + epb - 1) / epb;
+    const int grid = (int)std::min<int64_t>(groups, 16384);
+    if (ldim == 3)
+        hipLaunchKernelGGL(k_gradm1<3>, dim3(grid), dim3(threads), lds, S(stream), lx1, nel, epb, D, xm, ym, zm, u,
+                           ux, uy, uz);
+    else
+        hipLaunchKernelGGL(k_gradm1<2>, dim3(grid), dim3(threads), lds, S(stream), lx1, nel, epb, D, xm, ym, zm, u,
+                           ux, uy, uz);
+    NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+int nkv_bf_sensitivity(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe,
+                       const double* aIm, const double* grad, double* out, int ncomp, void* stream) {
+    CHECK(check_layout(L));
+    CHECK(check_ptr(dRe, "dRe"));
+    CHECK(check_ptr(dIm, "dIm"));
+    CHECK(check_ptr(aRe, "aRe"));
+    CHECK(check_ptr(aIm, "aIm"));
+    CHECK(check_ptr(grad, "grad"));
+    CHECK(check_ptr(out, "out"));
+    if (ncomp < 2 || ncomp > 3 || ncomp > L->n_wf)
+        return fail(NKV_EINVAL, "bf_sensitivity: ncomp=%d must be 2 or 3 and <= n_wf=%d", ncomp, L->n_wf);
+    if (L->n_v == 0) return NKV_OK;
+    auto kern = ncomp == 3 ? k_bf_sensitivity<3> : k_bf_sensitivity<2>;
+    hipLaunchKernelGGL(kern, dim3(grid_for(L->n_v)), dim3(kThreads), 0, S(stream), L->n_v, L->sv, dRe, dIm, aRe, aIm,
+                       grad, out);
     NKV_LAUNCHED();
     return NKV_OK;
 }

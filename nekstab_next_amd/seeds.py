@@ -95,6 +95,11 @@ class FaceAverage:
         self.start = torch.as_tensor(start).to(ctx.device)
         self.members = torch.as_tensor(members if members.size else np.zeros(1, np.int64)).to(ctx.device)
 
+    def apply(self, ptr: int) -> None:
+        """Average one field segment (n_v points at device address ``ptr``) in place."""
+        self.ctx.call_nl("nkv_group_average", self.n_groups, self.start.data_ptr(), self.members.data_ptr(), ptr,
+                         self.ctx.stream)
+
     def __call__(self, vec: NekVector, fields) -> None:
         ctx, lay = self.ctx, self.ctx.layout
         for f in fields:

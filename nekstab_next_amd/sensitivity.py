@@ -10,8 +10,16 @@ the adjoint mode (all fields incl. pressure and scalars; ``time`` untouched) so 
 ``ifto = ifpo = .false.``, :40), bi-orthogonalise them, form the pointwise product
 |u_d| |u_a| = sqrt(sum_c dRe_c^2 + dIm_c^2) sqrt(sum_c aRe_c^2 + aIm_c^2) (:69-71, one streaming
 kernel, ``nkv_wavemaker``) and write it as the temperature field of ``wm_<session>0.f00001``
-(:73-74).  It needs no derivatives.  The base-flow sensitivity (``bf_sensitivity``, :81-269) does
-— Nek5000's ``gradm1``/``dsavg`` on the spectral-element mesh — and stays out of scope.
+(:73-74).  It needs no derivatives.
+
+``bf_sensitivity`` (:81-269, Marquet et al.): the same four files and bi-orthogonalisation, then
+Nek5000's ``gradm1`` of every velocity component of the four modes (``nkv_gradm1``: one element per
+LDS tile, the geometric factors recomputed from the GLL coordinates on the fly, so a gradient reads
+the coordinates and the field once and writes its ldim components), ``dsavg`` of each gradient
+(direct-stiffness averaging: ``seeds.FaceAverage`` on one rank, the caller's gather-scatter on
+several), the pointwise terms tr, ti, pr, pi and sr = tr + pr, si = ti + pi in one streaming kernel
+(``nkv_bf_sensitivity``), written as the velocity of ``tr_``, ``ti_``, ``pr_``, ``pi_``, ``sr_``,
+``si_<session>0.f00001`` — the files ``ts_steady_force_sensitivity`` reads back (sr/si).
 
 ``ts_steady_force_sensitivity`` (:273-346): GMRES on the time-stepper form of the steady-force
 sensitivity problem, ``ts_gmres`` over the legacy dispatcher's mode-4 map; the forced Nek5000 run
@@ -79,6 +87,168 @@ def wavemaker_field(ctx: NekContext, dRe: NekVector, dIm: NekVector, aRe: NekVec
     return out
 
 
+def _load_modes(ctx: NekContext, directory: str, session: str, d_num: int, a_num: int, who: str):
+    """The four load_fld calls (sensitivity.f90:43-60, 143-160): dRe/dIm<session>0.f<d_num> and
+    aRe/aIm<session>0.f<a_num> into velocity-only device vectors (each rank its own elements).
+    Returns the vectors and the last file read (its time goes into the outputs' headers)."""
+    from . import fld
+
+    lay = ctx.layout
+    if lay.n_scalars or lay.n_p or lay.n_wf != lay.ldim:
+        raise ValueError(f"{who} works on a velocity-only context (sensitivity.velocity_layout)")
+    vecs, last = [], None
+    for prefix, num in (("dRe", d_num), ("dIm", d_num), ("aRe", a_num), ("aIm", a_num)):
+        files = fld.read_fld_set(directory, prefix, session, num)
+        if not files:
+            raise FileNotFoundError(f"{fld.fld_name(prefix, session, 0, num)} not found in {directory}")
+        last = files[0]
+        v = ctx.vector()
+        v.from_packed(fld.vector_from_fld(lay, files))
+        vecs.append(v)
+    return vecs, last
+
+
+def _out_file(lay: NekLayout, last, coords: dict | None):
+    """An empty field file of this rank's elements with the header of ``last`` (+ X if coords)."""
+    from . import fld
+
+    e0, e1 = lay.elem_range()
+    f = fld.FldFile(lay.lx1, lay.lx1, lay.lx1 if lay.ldim == 3 else 1, lay.nelgv, last.time, last.istep, lay.rank,
+                    lay.world, "", np.arange(e0 + 1, e1 + 1, dtype=np.int32), {})
+    if coords:
+        f.fields.update({k: np.asarray(v).reshape(lay.nelv, lay.pts_v) for k, v in coords.items()})
+        f.rdcode += "X"
+    return f
+
+
+def gll_derivative(n: int) -> np.ndarray:
+    """Nek5000's dxm1 (dgll): D[i, j] = P_N(z_i) / (P_N(z_j) (z_i - z_j)) for i != j,
+    D[0, 0] = -N(N+1)/4, D[N, N] = N(N+1)/4, zero elsewhere on the diagonal (row-major, n x n).
+    Nodes (Newton on P_N') and Legendre values in extended precision, then rounded: the matrix is
+    within an ulp of the exact one (a gradient amplifies D's error by the element's aspect)."""
+    from .fld import gll_points
+
+    ld = np.longdouble
+    N = n - 1
+
+    def legendre(x):   # P_N and P_N' by the three-term recurrence
+        p0, p1 = np.ones_like(x), x.copy()
+        if N == 0:
+            return p0, np.zeros_like(x)
+        for k in range(2, N + 1):
+            p0, p1 = p1, ((2 * k - 1) * x * p1 - (k - 1) * p0) / k
+        return p1, N * (x * p1 - p0) / (x * x - 1)
+
+    z = gll_points(n).astype(ld)
+    inner = z[1:-1].copy()
+    for _ in range(8):   # Newton on P_N'(z) = 0; P_N'' from Legendre's equation
+        p, dp = legendre(inner)
+        ddp = (2 * inner * dp - N * (N + 1) * p) / (1 - inner * inner)
+        inner = inner - dp / ddp
+    z[1:-1] = inner
+    with np.errstate(divide="ignore", invalid="ignore"):   # P_N' at the end points is not used
+        PN, _ = legendre(z)
+    PN[0], PN[-1] = ld((-1) ** N), ld(1)
+    D = np.zeros((n, n), dtype=ld)
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                D[i, j] = PN[i] / (PN[j] * (z[i] - z[j]))
+    D[0, 0] = ld(-N * (N + 1)) / 4
+    D[N, N] = ld(N * (N + 1)) / 4
+    return D.astype(np.float64)
+
+
+class Gradm1:
+    """Nek5000's ``gradm1`` on this rank's elements (``nkv_gradm1``): holds the GLL derivative
+    matrix and the coordinates {"x", "y"[, "z"]} (n_v each) on the device."""
+
+    def __init__(self, ctx: NekContext, coords: dict):
+        lay = ctx.layout
+        self.ctx = ctx
+        self.D = torch.as_tensor(gll_derivative(lay.lx1)).to(ctx.device)
+        self.xyz = []
+        for k in ("x", "y", "z")[: lay.ldim]:
+            a = np.asarray(coords[k], dtype=np.float64)
+            if a.size != lay.n_v:
+                raise ValueError(f"coords[{k!r}]: {a.size} points, the layout has n_v={lay.n_v}")
+            self.xyz.append(torch.as_tensor(a).to(ctx.device) if a.size else
+                            torch.zeros(1, dtype=torch.float64, device=ctx.device))
+
+    def __call__(self, u_ptr: int, out_ptrs) -> None:
+        """d(u)/dx, d(u)/dy[, d(u)/dz] of the field at ``u_ptr`` into ``out_ptrs`` (n_v doubles each)."""
+        lay = self.ctx.layout
+        three = lay.ldim == 3
+        self.ctx.call("nkv_gradm1", lay.lx1, lay.ldim, self.D.data_ptr(), self.xyz[0].data_ptr(),
+                      self.xyz[1].data_ptr(), self.xyz[2].data_ptr() if three else None, u_ptr, out_ptrs[0],
+                      out_ptrs[1], out_ptrs[2] if three else None, self.ctx.stream)
+
+
+BF_OUTPUTS = ("tr_", "ti_", "pr_", "pi_", "sr_", "si_")
+
+
+def bf_sensitivity_fields(ctx: NekContext, dRe: NekVector, dIm: NekVector, aRe: NekVector, aIm: NekVector,
+                          grad_op: Gradm1, face_average=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """sensitivity.f90:170-259 on bi-orthogonalised velocity-only vectors: gradm1 + dsavg of the
+    4 x ldim components (``face_average(ptr)`` averages one field segment in place; None skips
+    dsavg), then the pointwise terms.  Returns (out, grad): out holds 6 x ldim field segments
+    [tr, ti, pr, pi, sr, si][component], grad 4 x ldim x ldim [mode][component][direction]."""
+    lay = ctx.layout
+    d, sv = lay.ldim, lay.sv
+    grad = torch.zeros(4 * d * d * sv, dtype=torch.float64, device=ctx.device)
+    out = torch.zeros(6 * d * sv, dtype=torch.float64, device=ctx.device)
+    gp = grad.data_ptr()
+    for md, v in enumerate((dRe, dIm, aRe, aIm)):
+        for c in range(d):
+            ptrs = [gp + 8 * ((md * d + c) * d + k) * sv for k in range(d)]
+            grad_op(v.ptr + 8 * c * sv, ptrs)
+            if face_average is not None:
+                for q in ptrs:
+                    face_average(q)
+    ctx.call("nkv_bf_sensitivity", dRe.ptr, dIm.ptr, aRe.ptr, aIm.ptr, gp, out.data_ptr(), d, ctx.stream)
+    return out, grad
+
+
+def bf_sensitivity(ctx: NekContext, directory: str, coords: dict, session: str = "nek", d_num: int = 1,
+                   a_num: int = 2, outdir: str | None = None, face_average="auto", write_coords: bool = False) -> dict:
+    """``bf_sensitivity`` (sensitivity.f90:81-269) on a velocity-only context (``velocity_layout``):
+    the four mode files (as ``wave_maker``), ``biorthogonalize`` (:163-166), gradm1 + dsavg
+    (:170-199) and the terms (:202-235, 258-259) on the device, then ``outpost`` of the velocity of
+    tr_, ti_, pr_, pi_, sr_, si_<session><rank>.f00001 into ``outdir`` (default ``directory``;
+    ``ifto = ifpo = .false.``, :138; header time of the last file loaded).  ``coords``: this rank's
+    GLL coordinates (``seeds.coords_from_fld``).  ``face_average``: "auto" = one-rank averaging
+    over coincident points (``seeds.FaceAverage``; refused at world > 1), a callable ``f(ptr)``
+    (the case's gather-scatter on one field segment), or None (no dsavg).  Returns the six
+    outputs (this rank's points, [component] arrays), <adjoint, direct>_W and the files."""
+    from . import fld
+
+    lay = ctx.layout
+    (dRe, dIm, aRe, aIm), last = _load_modes(ctx, directory, session, d_num, a_num, "bf_sensitivity")
+    if isinstance(face_average, str):
+        if face_average != "auto":
+            raise ValueError("face_average: 'auto', a callable f(ptr) or None")
+        from .seeds import FaceAverage
+
+        face_average = FaceAverage(ctx, coords).apply
+    ip = biorthogonalize(ctx, dRe, dIm, aRe, aIm)
+    out, _ = bf_sensitivity_fields(ctx, dRe, dIm, aRe, aIm, Gradm1(ctx, coords), face_average)
+    ctx.check_nan()
+    host = out.view(6, lay.ldim, lay.sv)[:, :, : lay.n_v].cpu().numpy()
+    dst = outdir or directory
+    os.makedirs(dst, exist_ok=True)
+    result, paths = {}, []
+    for t, prefix in enumerate(BF_OUTPUTS):
+        f = _out_file(lay, last, coords if write_coords else None)
+        for c, nm in enumerate(("vx", "vy", "vz")[: lay.ldim]):
+            f.fields[nm] = host[t, c].reshape(lay.nelv, lay.pts_v)
+        f.rdcode += "U"
+        path = os.path.join(dst, fld.fld_name(prefix, session, lay.rank, 1))
+        fld.write_fld(path, f)
+        result[prefix.rstrip("_")] = [host[t, c].copy() for c in range(lay.ldim)]
+        paths.append(path)
+    return dict(fields=result, inner_product=ip, paths=paths, vectors=(dRe, dIm, aRe, aIm))
+
+
 def wave_maker(ctx: NekContext, directory: str, session: str = "nek", d_num: int = 1, a_num: int = 2,
                outdir: str | None = None, coords: dict | None = None) -> dict:
     """``wave_maker`` (sensitivity.f90:3-77) on a velocity-only context (``velocity_layout``).
@@ -95,26 +265,12 @@ def wave_maker(ctx: NekContext, directory: str, session: str = "nek", d_num: int
     from . import fld
 
     lay = ctx.layout
-    if lay.n_scalars or lay.n_p or lay.n_wf != lay.ldim:
-        raise ValueError("wave_maker works on a velocity-only context (sensitivity.velocity_layout)")
-    vecs, last = [], None
-    for prefix, num in (("dRe", d_num), ("dIm", d_num), ("aRe", a_num), ("aIm", a_num)):
-        files = fld.read_fld_set(directory, prefix, session, num)
-        last = files[0]
-        v = ctx.vector()
-        v.from_packed(fld.vector_from_fld(lay, files))
-        vecs.append(v)
-    dRe, dIm, aRe, aIm = vecs
+    (dRe, dIm, aRe, aIm), last = _load_modes(ctx, directory, session, d_num, a_num, "wave_maker")
     ip = biorthogonalize(ctx, dRe, dIm, aRe, aIm)
     wm_dev = wavemaker_field(ctx, dRe, dIm, aRe, aIm)
     ctx.check_nan()
     wm = wm_dev[: lay.n_v].cpu().numpy()
-    e0, e1 = lay.elem_range()
-    f = fld.FldFile(lay.lx1, lay.lx1, lay.lx1 if lay.ldim == 3 else 1, lay.nelgv, last.time, last.istep, lay.rank,
-                    lay.world, "", np.arange(e0 + 1, e1 + 1, dtype=np.int32), {})
-    if coords:
-        f.fields.update({k: np.asarray(v).reshape(lay.nelv, lay.pts_v) for k, v in coords.items()})
-        f.rdcode += "X"
+    f = _out_file(lay, last, coords)
     f.fields["t"] = wm.reshape(lay.nelv, lay.pts_v)
     f.rdcode += "T"
     out = outdir or directory

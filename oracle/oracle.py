@@ -9,7 +9,8 @@ What it restates (each function cites the reference line it follows):
   ordering rules ``quicksort2`` / ``select_eigenvalues`` / ``sort_eigendecomp``: plain C in
   ``nekstab_oracle.c`` (reference operation order, no FP contraction);
 * the drivers ``arnoldi_factorization``, ``krylov_schur``, ``schur_condensation``, ``eig``,
-  ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, the legacy ``matvec`` dispatcher,
+  ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, ``bf_sensitivity`` (with Nek5000's
+  ``gradm1``), the legacy ``matvec`` dispatcher,
   ``ts_steady_force_sensitivity``, ``newton_krylov``, the seed noise ``mth_rand`` with its
   direct-stiffness averaging: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
   dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
@@ -559,6 +560,159 @@ def wave_maker(L: OLayout, w, dRe, dIm, aRe, aIm):
     bi-orthogonalised vectors)."""
     vecs = biorthogonalize(L, w, dRe, dIm, aRe, aIm)
     return wavemaker_pointwise(L, *vecs), vecs
+
+
+def gll_derivative(n):
+    """The GLL derivative matrix D[i, m] = l_m'(z_i) (Nek5000's dxm1 from dgll), correctly rounded:
+    barycentric Lagrange differentiation at 60 digits (mpmath) on nodes refined at that precision
+    from the oracle's own (``nekio._gll_nodes``) — an independent route to the matrix the product
+    builds from Legendre values in extended precision."""
+    import mpmath
+    from nekio import _gll_nodes
+
+    with mpmath.workdps(60):
+        N = n - 1
+        dP = lambda x: mpmath.diff(lambda t: mpmath.legendre(N, t), x)  # noqa: E731
+        z = [mpmath.mpf(-1)] + [mpmath.findroot(dP, mpmath.mpf(float(a))) for a in _gll_nodes(n)[1:-1]] + [mpmath.mpf(1)]
+        w = [1 / mpmath.fprod([z[i] - z[j] for j in range(n) if j != i]) for i in range(n)]
+        D = np.zeros((n, n))
+        for i in range(n):
+            row = [(w[m] / w[i]) / (z[i] - z[m]) if m != i else mpmath.mpf(0) for m in range(n)]
+            row[i] = -mpmath.fsum(row)
+            D[i] = [float(v) if abs(v) > 1e-40 else 0.0 for v in row]   # interior diagonal: 0
+    return D
+
+
+def _mxm_r(D, A):
+    """d/dr of element-major (nel, nz, ny, nx) data: sum_m D[i, m] A[..., m], m ascending (mxm)."""
+    out = D[None, None, None, :, 0] * A[..., 0:1]
+    for m in range(1, A.shape[-1]):
+        out = out + D[None, None, None, :, m] * A[..., m:m + 1]
+    return out
+
+
+def _mxm_s(D, A):
+    out = A[:, :, 0:1, :] * D[None, None, :, 0, None]
+    for m in range(1, A.shape[2]):
+        out = out + A[:, :, m:m + 1, :] * D[None, None, :, m, None]
+    return out
+
+
+def _mxm_t(D, A):
+    out = A[:, 0:1] * D[None, :, 0, None, None]
+    for m in range(1, A.shape[1]):
+        out = out + A[:, m:m + 1] * D[None, :, m, None, None]
+    return out
+
+
+def gradm1(lx1, ldim, coords, u):
+    """Nek5000's gradm1 (navier5.f; not in the reference tree, called at sensitivity.f90:170-199)
+    with the geometric factors of its glmapm1 / xyzrst (coef.f), restated from the published
+    source: xr = D x along r (mxm), xs, xt along s, t; 2-D jac = xr ys - xs yr, rx = ys, ry = -xs,
+    sx = -yr, sy = xr; 3-D jac by addcol4 / subcol4 and the cofactors by ascol5; ux = (1/jac)
+    (ur rx + us sx [+ ut tx]).  Element-major points (n_v), one field.  Returns [ux, uy(, uz)]."""
+    D = gll_derivative(lx1)
+    nz = lx1 if ldim == 3 else 1
+    shp = (-1, nz, lx1, lx1)
+    X, Y, U = (np.asarray(a, dtype=np.float64).reshape(shp) for a in (coords["x"], coords["y"], u))
+    xr, yr, ur = _mxm_r(D, X), _mxm_r(D, Y), _mxm_r(D, U)
+    xs, ys, us = _mxm_s(D, X), _mxm_s(D, Y), _mxm_s(D, U)
+    if ldim == 2:
+        jac = 0.0 + xr * ys
+        jac = jac - xs * yr
+        rx, ry, sx, sy = ys, -xs, -yr, xr
+        jacmi = 1.0 / jac
+        return [(jacmi * (ur * rx + us * sx)).ravel(), (jacmi * (ur * ry + us * sy)).ravel()]
+    Z = np.asarray(coords["z"], dtype=np.float64).reshape(shp)
+    zr, zs = _mxm_r(D, Z), _mxm_s(D, Z)
+    xt, yt, zt, ut = _mxm_t(D, X), _mxm_t(D, Y), _mxm_t(D, Z), _mxm_t(D, U)
+    jac = 0.0 + xr * ys * zt
+    jac = jac + xt * yr * zs
+    jac = jac + xs * yt * zr
+    jac = jac - xr * yt * zs
+    jac = jac - xs * yr * zt
+    jac = jac - xt * ys * zr
+    rx, ry, rz = ys * zt - yt * zs, xt * zs - xs * zt, xs * yt - xt * ys
+    sx, sy, sz = yt * zr - yr * zt, xr * zt - xt * zr, xt * yr - xr * yt
+    tx, ty, tz = yr * zs - ys * zr, xs * zr - xr * zs, xr * ys - xs * yr
+    jacmi = 1.0 / jac
+    return [(jacmi * (ur * rx + us * sx + ut * tx)).ravel(), (jacmi * (ur * ry + us * sy + ut * ty)).ravel(),
+            (jacmi * (ur * rz + us * sz + ut * tz)).ravel()]
+
+
+def bf_sensitivity_terms(ldim, d_re, d_im, a_re, a_im, g):
+    """sensitivity.f90:202-235, 258-259 line by line.  d_re ... : lists of velocity components
+    [vx, vy(, vz)]; g[(mode, comp, dir)] the dsavg'd gradients, mode in 'dRe','dIm','aRe','aIm',
+    comp in 'u','v','w', dir in 'x','y','z'.  opaddcol3(a1,a2,a3,b1,b2,b3,c1,c2,c3) is
+    a_c = a_c + b_c*c_c with a3 only in 3-D.  The 2-D reference reads vz_* / dw* arrays it never set
+    (opcopy skips vz, gradm1 skips z): those terms are absent here.  Returns dict tr, ti, pr, pi,
+    sr, si of component lists."""
+    n = d_re[0].size
+    three = ldim == 3
+
+    def G(md, c, d):
+        return g.get((md, c, d))
+
+    def opaddcol3(a, b, c1, c2, c3):
+        if b is None:            # a vz_* multiplier in 2-D: the never-set array, absent
+            return
+        a[0] = a[0] + b * c1
+        a[1] = a[1] + b * c2
+        if three:
+            a[2] = a[2] + b * c3
+
+    vz = lambda v: v[2] if three else None  # noqa: E731
+    neg = lambda v: None if v is None else -v  # noqa: E731
+    tr = [np.zeros(n) for _ in range(ldim)]
+    opaddcol3(tr, -a_re[0], G("dRe", "u", "x"), G("dRe", "u", "y"), G("dRe", "u", "z"))
+    opaddcol3(tr, -a_re[1], G("dRe", "v", "x"), G("dRe", "v", "y"), G("dRe", "w", "z"))
+    opaddcol3(tr, neg(vz(a_re)), G("dRe", "w", "x"), G("dRe", "w", "y"), G("dRe", "w", "z"))
+    opaddcol3(tr, -a_im[0], G("dIm", "u", "x"), G("dIm", "u", "y"), G("dIm", "u", "z"))
+    opaddcol3(tr, -a_im[1], G("dIm", "v", "x"), G("dIm", "v", "y"), G("dIm", "w", "z"))
+    opaddcol3(tr, neg(vz(a_im)), G("dIm", "w", "x"), G("dIm", "w", "y"), G("dIm", "w", "z"))
+    ti = [np.zeros(n) for _ in range(ldim)]
+    opaddcol3(ti, a_re[0], G("dIm", "u", "x"), G("dIm", "u", "y"), G("dIm", "u", "z"))
+    opaddcol3(ti, a_re[1], G("dIm", "v", "x"), G("dIm", "v", "y"), G("dIm", "w", "z"))
+    opaddcol3(ti, vz(a_re), G("dIm", "w", "x"), G("dIm", "w", "y"), G("dIm", "w", "z"))
+    opaddcol3(ti, -a_im[0], G("dRe", "u", "x"), G("dRe", "u", "y"), G("dRe", "u", "z"))
+    opaddcol3(ti, -a_im[1], G("dRe", "v", "x"), G("dRe", "v", "y"), G("dRe", "w", "z"))
+    opaddcol3(ti, neg(vz(a_im)), G("dRe", "w", "x"), G("dRe", "w", "y"), G("dRe", "w", "z"))
+    pr = [np.zeros(n) for _ in range(ldim)]
+    opaddcol3(pr, d_re[0], G("aRe", "u", "x"), G("aRe", "v", "x"), G("aRe", "w", "x"))
+    opaddcol3(pr, d_re[1], G("aRe", "u", "y"), G("aRe", "v", "y"), G("aRe", "w", "y"))
+    opaddcol3(pr, vz(d_re), G("aRe", "u", "z"), G("aRe", "v", "z"), G("aRe", "w", "z"))
+    opaddcol3(pr, d_im[0], G("aIm", "u", "x"), G("aIm", "v", "x"), G("aIm", "w", "x"))
+    opaddcol3(pr, d_im[1], G("aIm", "u", "y"), G("aIm", "v", "y"), G("aIm", "w", "y"))
+    opaddcol3(pr, vz(d_im), G("aIm", "u", "z"), G("aIm", "v", "z"), G("aIm", "w", "z"))
+    pi = [np.zeros(n) for _ in range(ldim)]
+    opaddcol3(pi, d_re[0], G("aIm", "u", "x"), G("aIm", "v", "x"), G("aIm", "w", "x"))
+    opaddcol3(pi, d_re[1], G("aIm", "u", "y"), G("aIm", "v", "y"), G("aIm", "w", "y"))
+    opaddcol3(pi, vz(d_re), G("aIm", "u", "z"), G("aIm", "v", "z"), G("aIm", "w", "z"))
+    opaddcol3(pi, -d_im[0], G("aRe", "u", "x"), G("aRe", "v", "x"), G("aRe", "w", "x"))
+    opaddcol3(pi, -d_im[1], G("aRe", "u", "y"), G("aRe", "v", "y"), G("aRe", "w", "y"))
+    opaddcol3(pi, neg(vz(d_im)), G("aRe", "u", "z"), G("aRe", "v", "z"), G("aRe", "w", "z"))
+    sr = [tr[c] + pr[c] for c in range(ldim)]      # opadd2, :258
+    si = [ti[c] + pi[c] for c in range(ldim)]      # :259
+    return dict(tr=tr, ti=ti, pr=pr, pi=pi, sr=sr, si=si)
+
+
+def bf_sensitivity(L: OLayout, w, lx1, coords, dRe, dIm, aRe, aIm, average=None):
+    """sensitivity.f90:81-269 after the four load_fld calls (``ifto = ifpo = .false.``, :138: ``L``
+    is the velocity-only layout): biorthogonalize (:163-166), gradm1 + dsavg of every velocity
+    component of the four modes (:170-199; ``average(q)`` is dsavg, default the one-rank
+    ``coincident_average``), then the pointwise terms (``bf_sensitivity_terms``).  Reference-order
+    vectors.  Returns (terms, the four bi-orthogonalised vectors, the gradients)."""
+    if average is None:
+        average = lambda q: coincident_average(q, coords)  # noqa: E731
+    vecs = biorthogonalize(L, w, dRe, dIm, aRe, aIm)
+    nv, ldim = L.nv, L.ldim
+    comps = [[v[c * nv:(c + 1) * nv] for c in range(ldim)] for v in vecs]
+    g = {}
+    for md, vc in zip(("dRe", "dIm", "aRe", "aIm"), comps):
+        for c, cn in enumerate("uvw"[:ldim]):
+            for d, dn in zip(range(ldim), gradm1(lx1, ldim, coords, vc[c])):
+                g[(md, cn, "xyz"[d])] = average(dn)
+    return bf_sensitivity_terms(ldim, *comps, g), vecs, g
 
 
 def _cr(fn):
