@@ -392,15 +392,18 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
                   double* out, int ncomp, void* stream);
 /* bf_sensitivity (sensitivity.f90:81-269), the base-flow sensitivity of Marquet et al.:
  * nkv_gradm1: Nek5000's gradm1 (the calls at sensitivity.f90:170-199; navier5.f, with glmapm1 /
- * xyzrst's geometric factors from the GLL coordinates xm, ym, [zm]) of one field u (n_v points,
- * Nek point order, lx1^ldim per element) into ux, uy, [uz]; D is the lx1 x lx1 GLL derivative matrix
- * (row-major D[i*lx1+m] = l_m'(z_i), device).  Element-local.  zm and uz exactly when ldim = 3.
+ * xyzrst's geometric factors from the GLL coordinates xm, ym, [zm]) of nfld fields (field f: n_v
+ * points at u + f*u_stride, Nek point order, lx1^ldim per element, lx1 <= 10) into
+ * grad + (f*ldim + d)*g_stride for direction d = x, y, [z]; the geometric factors are formed once
+ * for all nfld fields.  D is the lx1 x lx1 GLL derivative matrix (row-major D[i*lx1+m] = l_m'(z_i),
+ * device).  Element-local.  zm exactly when ldim = 3.
  * nkv_bf_sensitivity: the pointwise terms (:202-235) and their sums (:258-259) after gradm1 + dsavg:
  * grad = 4*ncomp*ncomp field segments [dRe, dIm, aRe, aIm][u, v, w][x, y, z] (sv doubles each),
  * out = 6*ncomp segments [tr, ti, pr, pi, sr, si][component].  The reference's dwdz-for-dvdz slips
  * (:204, 207, 213, 216) are kept; its 2-D reads of never-set vz arrays are absent. */
 int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const double* xm, const double* ym,
-               const double* zm, const double* u, double* ux, double* uy, double* uz, void* stream);
+               const double* zm, const double* u, int nfld, int64_t u_stride, double* grad, int64_t g_stride,
+               void* stream);
 int nkv_bf_sensitivity(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe,
                        const double* aIm, const double* grad, double* out, int ncomp, void* stream);
 

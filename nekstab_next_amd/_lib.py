@@ -113,7 +113,7 @@ _SIGNATURES = {
     "nkv_group_average": (c_int, [c_int64, _P, _P, _P, _P]),
     "nkv_symmetric_seed": (c_int, [_L, _P, _P, c_double, _P, _P, _P, _P]),
     "nkv_wavemaker": (c_int, [_L, _P, _P, _P, _P, _P, c_int, _P]),
-    "nkv_gradm1": (c_int, [_L, c_int, c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "nkv_gradm1": (c_int, [_L, c_int, c_int, _P, _P, _P, _P, _P, c_int, c_int64, _P, c_int64, _P]),
     "nkv_bf_sensitivity": (c_int, [_L, _P, _P, _P, _P, _P, _P, c_int, _P]),
     "nkv_givens_column": (c_double, [c_int, _P, _P, _P, _P]),
     "nkv_gkl_coef": (c_int, [c_int, c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P]),

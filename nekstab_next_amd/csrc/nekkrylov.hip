@@ -1950,28 +1950,44 @@ int launch_block_update_p(const nkv_layout* L, const double* w, const double* Q,
 //   3-D: jac = xr ys zt + xt yr zs + xs yt zr - xr yt zs - xs yr zt - xt ys zr (addcol4 / subcol4),
 //        rx = ys zt - yt zs, ry = xt zs - xs zt, rz = xs yt - xt ys, sx = yt zr - yr zt, ...  (ascol5)
 //   ux = (1/jac) (ur rx + us sx [+ ut tx]),  uy, uz likewise
-// One workgroup holds `epb` whole elements in LDS (coordinates, u, D); each thread owns one point.
-// No contraction (the reference's operand order).  Element-local: it shards with the elements.
-template <int LDIM>
-__global__ __launch_bounds__(1024) void k_gradm1(int nx, int64_t nel, int epb, const double* __restrict__ Dg,
+// One workgroup holds `epb` whole elements in LDS; each thread owns one point, keeps its rows of D
+// and its geometric factors in registers and differentiates NFLD fields (field f at u + f u_stride)
+// against them, so the coordinates are read and the factors formed once per launch, not per field.
+// NX (= lx1) is a template parameter; the line sums are unrolled by 2 (full unrolling hoists every
+// LDS read into registers: 228 VGPRs at lx1=8 in 3-D, 2 waves per SIMD and 1.6x slower; by 1 or 4
+// within 2-7 %, profiles/r03bh_gradm1_variants.log).  No contraction (the reference's operand order).
+// Element-local: it shards with the elements.
+template <int LDIM, int NX>
+constexpr int gradm1_threads() {   // whole elements per workgroup, whole waves
+    return (LDIM == 3 ? NX * NX * NX : NX * NX) >= 256 ? ((LDIM == 3 ? NX * NX * NX : NX * NX) + 63) / 64 * 64 : 256;
+}
+
+template <int LDIM, int NX>
+__global__ __launch_bounds__((gradm1_threads<LDIM, NX>())) void k_gradm1(int64_t nel, int epb, int nfld, const double* __restrict__ Dg,
                                                  const double* __restrict__ xm, const double* __restrict__ ym,
                                                  const double* __restrict__ zm, const double* __restrict__ u,
-                                                 double* __restrict__ ux, double* __restrict__ uy,
-                                                 double* __restrict__ uz) {
+                                                 int64_t u_stride, double* __restrict__ grad, int64_t g_stride) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
-    const int pts = LDIM == 3 ? nx * nx * nx : nx * nx;
+    constexpr int pts = LDIM == 3 ? NX * NX * NX : NX * NX;
+    constexpr int sj = NX, sk = NX * NX;     // strides of s and t inside an element
     const int nt = epb * pts;
-    double* D = lds;
-    double* X = D + nx * nx;
+    double* D = lds;                         // D(i, m) at D[i*NX + m]
+    double* X = D + NX * NX;
     double* Y = X + nt;
-    double* Z = Y + nt;              // 3-D only
+    double* Z = Y + nt;                      // 3-D only
     double* U = LDIM == 3 ? Z + nt : Z;
-    for (int t = threadIdx.x; t < nx * nx; t += blockDim.x) D[t] = Dg[t];
     const int tid = threadIdx.x;
+    for (int t = tid; t < NX * NX; t += blockDim.x) D[t] = Dg[t];
     const int le = tid / pts, r = tid - le * pts;
-    const int i = r % nx, j = (r / nx) % nx, k = LDIM == 3 ? r / (nx * nx) : 0;
+    const int i = r % NX, j = (r / NX) % NX, k = LDIM == 3 ? r / (NX * NX) : 0;
     const int base = le * pts;
+    const int ri = base + j * sj + k * sk;   // line along r through (., j, k)
+    const int si = base + i + k * sk;        // line along s through (i, ., k)
+    const int ti = base + i + j * sj;        // line along t through (i, j, .)
+    const double* Di = D + i * NX;           // this point's rows of D (LDS)
+    const double* Dj = D + j * NX;
+    const double* Dk = D + k * NX;
     for (int64_t e0 = (int64_t)blockIdx.x * epb; e0 < nel; e0 += (int64_t)gridDim.x * epb) {
         const int64_t p = e0 * pts + tid;
         const bool live = tid < nt && e0 + le < nel;
@@ -1980,45 +1996,38 @@ __global__ __launch_bounds__(1024) void k_gradm1(int nx, int64_t nel, int epb, c
             X[tid] = xm[p];
             Y[tid] = ym[p];
             if (LDIM == 3) Z[tid] = zm[p];
-            U[tid] = u[p];
         }
         __syncthreads();
-        if (!live) continue;
-        const int sj = nx, sk = nx * nx;            // strides of s and t inside an element
-        const int ri = base + j * sj + k * sk;      // line along r through (., j, k)
-        const int si = base + i + k * sk;           // line along s through (i, ., k)
-        const int ti = base + i + j * sj;           // line along t through (i, j, .)
-        const double* Di = D + i * nx;
-        const double* Dj = D + j * nx;
-        double xr = Di[0] * X[ri], yr = Di[0] * Y[ri], ur = Di[0] * U[ri];
-        double xs = X[si] * Dj[0], ys = Y[si] * Dj[0], us = U[si] * Dj[0];
-        for (int m = 1; m < nx; ++m) {
+        // geometric factors of this point (registers; dead lanes compute garbage they never store)
+        double xr = Di[0] * X[ri], yr = Di[0] * Y[ri];
+        double xs = X[si] * Dj[0], ys = Y[si] * Dj[0];
+#pragma unroll 2
+        for (int m = 1; m < NX; ++m) {
             xr = xr + Di[m] * X[ri + m];
             yr = yr + Di[m] * Y[ri + m];
-            ur = ur + Di[m] * U[ri + m];
             xs = xs + X[si + m * sj] * Dj[m];
             ys = ys + Y[si + m * sj] * Dj[m];
-            us = us + U[si + m * sj] * Dj[m];
         }
+        double g[3][3], jacmi;   // g[direction][reference coordinate r, s, t]
         if constexpr (LDIM == 2) {
             double jac = 0.0;
             jac = jac + xr * ys;
             jac = jac - xs * yr;
-            const double rx = ys, ry = -xs, sx = -yr, sy = xr;
-            const double jacmi = 1.0 / jac;
-            ux[p] = jacmi * (ur * rx + us * sx);
-            uy[p] = jacmi * (ur * ry + us * sy);
+            g[0][0] = ys;
+            g[1][0] = -xs;
+            g[0][1] = -yr;
+            g[1][1] = xr;
+            jacmi = 1.0 / jac;
         } else {
-            const double* Dk = D + k * nx;
             double zr = Di[0] * Z[ri], zs = Z[si] * Dj[0];
-            double xt = X[ti] * Dk[0], yt = Y[ti] * Dk[0], zt = Z[ti] * Dk[0], ut = U[ti] * Dk[0];
-            for (int m = 1; m < nx; ++m) {
+            double xt = X[ti] * Dk[0], yt = Y[ti] * Dk[0], zt = Z[ti] * Dk[0];
+#pragma unroll 2
+            for (int m = 1; m < NX; ++m) {
                 zr = zr + Di[m] * Z[ri + m];
                 zs = zs + Z[si + m * sj] * Dj[m];
                 xt = xt + X[ti + m * sk] * Dk[m];
                 yt = yt + Y[ti + m * sk] * Dk[m];
                 zt = zt + Z[ti + m * sk] * Dk[m];
-                ut = ut + U[ti + m * sk] * Dk[m];
             }
             double jac = 0.0;
             jac = jac + xr * ys * zt;
@@ -2027,13 +2036,41 @@ __global__ __launch_bounds__(1024) void k_gradm1(int nx, int64_t nel, int epb, c
             jac = jac - xr * yt * zs;
             jac = jac - xs * yr * zt;
             jac = jac - xt * ys * zr;
-            const double rx = ys * zt - yt * zs, ry = xt * zs - xs * zt, rz = xs * yt - xt * ys;
-            const double sx = yt * zr - yr * zt, sy = xr * zt - xt * zr, sz = xt * yr - xr * yt;
-            const double tx = yr * zs - ys * zr, ty = xs * zr - xr * zs, tz = xr * ys - xs * yr;
-            const double jacmi = 1.0 / jac;
-            ux[p] = jacmi * (ur * rx + us * sx + ut * tx);
-            uy[p] = jacmi * (ur * ry + us * sy + ut * ty);
-            uz[p] = jacmi * (ur * rz + us * sz + ut * tz);
+            g[0][0] = ys * zt - yt * zs;   // rx
+            g[1][0] = xt * zs - xs * zt;   // ry
+            g[2][0] = xs * yt - xt * ys;   // rz
+            g[0][1] = yt * zr - yr * zt;   // sx
+            g[1][1] = xr * zt - xt * zr;   // sy
+            g[2][1] = xt * yr - xr * yt;   // sz
+            g[0][2] = yr * zs - ys * zr;   // tx
+            g[1][2] = xs * zr - xr * zs;   // ty
+            g[2][2] = xr * ys - xs * yr;   // tz
+            jacmi = 1.0 / jac;
+        }
+        for (int f = 0; f < nfld; ++f) {
+            if (f > 0) __syncthreads();   // every lane is done reading the previous field
+            if (live) U[tid] = u[f * u_stride + p];
+            __syncthreads();
+            if (live) {
+                double ur = Di[0] * U[ri], us = U[si] * Dj[0], ut = 0.0;
+#pragma unroll 2
+                for (int m = 1; m < NX; ++m) {
+                    ur = ur + Di[m] * U[ri + m];
+                    us = us + U[si + m * sj] * Dj[m];
+                }
+                if constexpr (LDIM == 3) {
+                    ut = U[ti] * Dk[0];
+#pragma unroll 2
+                    for (int m = 1; m < NX; ++m) ut = ut + U[ti + m * sk] * Dk[m];
+                }
+                double* out = grad + (int64_t)f * LDIM * g_stride + p;
+#pragma unroll
+                for (int d = 0; d < LDIM; ++d) {
+                    const double acc = LDIM == 3 ? ur * g[d][0] + us * g[d][1] + ut * g[d][2]
+                                                 : ur * g[d][0] + us * g[d][1];
+                    out[d * g_stride] = jacmi * acc;
+                }
+            }
         }
     }
 }
@@ -2106,6 +2143,19 @@ __global__ __launch_bounds__(kThreads) void k_bf_sensitivity(int64_t n, int64_t 
             out[(5 * LDIM + c) * sv + p] = ti[c] + pi[c];   // :259
         }
     }
+}
+
+template <int LDIM, int NX>
+static void launch_gradm1(int64_t nel, int nfld, const double* D, const double* xm, const double* ym, const double* zm,
+                          const double* u, int64_t u_stride, double* grad, int64_t g_stride, void* stream) {
+    constexpr int pts = LDIM == 3 ? NX * NX * NX : NX * NX;
+    const int epb = pts >= 256 ? 1 : 256 / pts;             // whole elements per workgroup
+    const int threads = gradm1_threads<LDIM, NX>();
+    const size_t lds = sizeof(double) * ((size_t)NX * NX + (size_t)(LDIM + 1) * epb * pts);
+    const int64_t groups = (nel + epb - 1) / epb;
+    const int grid = (int)std::min<int64_t>(groups, 16384);
+    hipLaunchKernelGGL((k_gradm1<LDIM, NX>), dim3(grid), dim3(threads), lds, S(stream), nel, epb, nfld, D, xm, ym, zm,
+                       u, u_stride, grad, g_stride);
 }
 
 extern "C" {
@@ -3462,7 +3512,8 @@ int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, con
 }
 
 int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const double* xm, const double* ym,
-               const double* zm, const double* u, double* ux, double* uy, double* uz, void* stream) {
+               const double* zm, const double* u, int nfld, int64_t u_stride, double* grad, int64_t g_stride,
+               void* stream) {
     CHECK(check_layout(L));
     if (ldim != 2 && ldim != 3) return fail(NKV_EINVAL, "gradm1: ldim=%d must be 2 or 3", ldim);
     if (lx1 < 2 || lx1 > 10) return fail(NKV_EINVAL, "gradm1: lx1=%d outside 2..10", lx1);
@@ -3470,26 +3521,34 @@ int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const do
     if (L->n_v % pts != 0)
         return fail(NKV_EINVAL, "gradm1: %d points per element do not divide n_v=%lld", pts, (long long)L->n_v);
     if ((ldim == 3) != (zm != nullptr)) return fail(NKV_EINVAL, "gradm1: zm must be given exactly in 3-D");
-    if ((ldim == 3) != (uz != nullptr)) return fail(NKV_EINVAL, "gradm1: uz must be given exactly in 3-D");
+    if (nfld < 1) return fail(NKV_EINVAL, "gradm1: nfld=%d < 1", nfld);
+    if ((nfld > 1 && u_stride < L->n_v) || g_stride < L->n_v)
+        return fail(NKV_EINVAL, "gradm1: strides u=%lld g=%lld below n_v=%lld", (long long)u_stride,
+                    (long long)g_stride, (long long)L->n_v);
     CHECK(check_ptr(D, "D"));
     CHECK(check_ptr(xm, "xm"));
     CHECK(check_ptr(ym, "ym"));
     CHECK(check_ptr(u, "u"));
-    CHECK(check_ptr(ux, "ux"));
-    CHECK(check_ptr(uy, "uy"));
+    CHECK(check_ptr(grad, "grad"));
     const int64_t nel = L->n_v / pts;
     if (nel == 0) return NKV_OK;
-    const int epb = pts >= 256 ? 1 : 256 / pts;            // whole elements per workgroup
-    const int threads = ((epb * pts + 63) / 64) * 64;       // whole waves
-    const size_t lds = sizeof(double) * ((size_t)lx1 * lx1 + (size_t)(ldim + 1) * epb * pts);
-    const int64_t groups = (nel + epb - 1) / epb;
-    const int grid = (int)std::min<int64_t>(groups, 16384);
-    if (ldim == 3)
-        hipLaunchKernelGGL(k_gradm1<3>, dim3(grid), dim3(threads), lds, S(stream), lx1, nel, epb, D, xm, ym, zm, u,
-                           ux, uy, uz);
-    else
-        hipLaunchKernelGGL(k_gradm1<2>, dim3(grid), dim3(threads), lds, S(stream), lx1, nel, epb, D, xm, ym, zm, u,
-                           ux, uy, uz);
+#define NKV_GRADM1_CASE(NX)                                                                                   \
+    case NX:                                                                                                  \
+        if (ldim == 3) launch_gradm1<3, NX>(nel, nfld, D, xm, ym, zm, u, u_stride, grad, g_stride, stream);  \
+        else launch_gradm1<2, NX>(nel, nfld, D, xm, ym, zm, u, u_stride, grad, g_stride, stream);            \
+        break;
+    switch (lx1) {
+        NKV_GRADM1_CASE(2)
+        NKV_GRADM1_CASE(3)
+        NKV_GRADM1_CASE(4)
+        NKV_GRADM1_CASE(5)
+        NKV_GRADM1_CASE(6)
+        NKV_GRADM1_CASE(7)
+        NKV_GRADM1_CASE(8)
+        NKV_GRADM1_CASE(9)
+        NKV_GRADM1_CASE(10)
+    }
+#undef NKV_GRADM1_CASE
     NKV_LAUNCHED();
     return NKV_OK;
 }

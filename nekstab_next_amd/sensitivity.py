@@ -175,13 +175,15 @@ class Gradm1:
             self.xyz.append(torch.as_tensor(a).to(ctx.device) if a.size else
                             torch.zeros(1, dtype=torch.float64, device=ctx.device))
 
-    def __call__(self, u_ptr: int, out_ptrs) -> None:
-        """d(u)/dx, d(u)/dy[, d(u)/dz] of the field at ``u_ptr`` into ``out_ptrs`` (n_v doubles each)."""
+    def __call__(self, u_ptr: int, grad_ptr: int, nfld: int = 1, u_stride: int = 0, g_stride: int | None = None) -> None:
+        """Gradients of ``nfld`` fields (field f: n_v doubles at ``u_ptr + 8 f u_stride``) into
+        ``grad_ptr + 8 (f ldim + d) g_stride`` (d = x, y[, z]; ``g_stride`` default n_v); the
+        geometric factors are formed once for all of them."""
         lay = self.ctx.layout
         three = lay.ldim == 3
         self.ctx.call("nkv_gradm1", lay.lx1, lay.ldim, self.D.data_ptr(), self.xyz[0].data_ptr(),
-                      self.xyz[1].data_ptr(), self.xyz[2].data_ptr() if three else None, u_ptr, out_ptrs[0],
-                      out_ptrs[1], out_ptrs[2] if three else None, self.ctx.stream)
+                      self.xyz[1].data_ptr(), self.xyz[2].data_ptr() if three else None, u_ptr, int(nfld),
+                      int(u_stride), grad_ptr, int(lay.n_v if g_stride is None else g_stride), self.ctx.stream)
 
 
 BF_OUTPUTS = ("tr_", "ti_", "pr_", "pi_", "sr_", "si_")
@@ -198,13 +200,11 @@ def bf_sensitivity_fields(ctx: NekContext, dRe: NekVector, dIm: NekVector, aRe: 
     grad = torch.zeros(4 * d * d * sv, dtype=torch.float64, device=ctx.device)
     out = torch.zeros(6 * d * sv, dtype=torch.float64, device=ctx.device)
     gp = grad.data_ptr()
-    for md, v in enumerate((dRe, dIm, aRe, aIm)):
-        for c in range(d):
-            ptrs = [gp + 8 * ((md * d + c) * d + k) * sv for k in range(d)]
-            grad_op(v.ptr + 8 * c * sv, ptrs)
-            if face_average is not None:
-                for q in ptrs:
-                    face_average(q)
+    for md, v in enumerate((dRe, dIm, aRe, aIm)):   # one launch per mode: its d components together
+        grad_op(v.ptr, gp + 8 * md * d * d * sv, nfld=d, u_stride=sv, g_stride=sv)
+    if face_average is not None:
+        for q in range(4 * d * d):
+            face_average(gp + 8 * q * sv)
     ctx.call("nkv_bf_sensitivity", dRe.ptr, dIm.ptr, aRe.ptr, aIm.ptr, gp, out.data_ptr(), d, ctx.stream)
     return out, grad
 

@@ -40,10 +40,10 @@ def _grad_device(ctx, coords, u):
     lay = ctx.layout
     op = Gradm1(ctx, coords)
     ut = torch.as_tensor(np.asarray(u, dtype=np.float64)).to(ctx.device)
-    outs = [torch.full((lay.n_v,), np.nan, dtype=torch.float64, device=ctx.device) for _ in range(lay.ldim)]
-    op(ut.data_ptr(), [o.data_ptr() for o in outs])
+    out = torch.full((lay.ldim, lay.n_v), np.nan, dtype=torch.float64, device=ctx.device)
+    op(ut.data_ptr(), out.data_ptr())
     torch.cuda.synchronize()
-    return [o.cpu().numpy() for o in outs]
+    return list(out.cpu().numpy())
 
 
 def _cases():
@@ -82,20 +82,43 @@ def test_gradm1_argument_checks(gpu):
     co = box_mesh_coords(lay, (2, 1, 1))
     op = Gradm1(ctx, co)
     u = torch.zeros(lay.n_v, dtype=torch.float64, device=ctx.device)
-    o = [torch.zeros(lay.n_v, dtype=torch.float64, device=ctx.device) for _ in range(3)]
+    o = torch.zeros(3 * lay.n_v, dtype=torch.float64, device=ctx.device)
     xp = [t.data_ptr() for t in op.xyz]
-    lib = ctx.lib
-    assert lib.nkv_gradm1(ctx._Lp, 5, 4, op.D.data_ptr(), *xp, u.data_ptr(), *(t.data_ptr() for t in o),
-                          ctx.stream) == _lib.NKV_EINVAL
-    assert lib.nkv_gradm1(ctx._Lp, 5, 3, op.D.data_ptr(), xp[0], xp[1], None, u.data_ptr(),
-                          *(t.data_ptr() for t in o), ctx.stream) == _lib.NKV_EINVAL
-    assert "zm" in _lib.last_error()
-    assert lib.nkv_gradm1(ctx._Lp, 6, 3, op.D.data_ptr(), *xp, u.data_ptr(), *(t.data_ptr() for t in o),
-                          ctx.stream) == _lib.NKV_EINVAL      # 216 points per element do not divide n_v
-    assert lib.nkv_gradm1(ctx._Lp, 11, 3, op.D.data_ptr(), *xp, u.data_ptr(), *(t.data_ptr() for t in o),
-                          ctx.stream) == _lib.NKV_EINVAL
+    lib, D, n = ctx.lib, op.D.data_ptr(), lay.n_v
+
+    def call(lx1, ldim, x=xp, nfld=1, us=0, gs=n, grad=o.data_ptr()):
+        return lib.nkv_gradm1(ctx._Lp, lx1, ldim, D, *x, u.data_ptr(), nfld, us, grad, gs, ctx.stream)
+
+    assert call(5, 3) == _lib.NKV_OK
+    assert call(5, 4) == _lib.NKV_EINVAL
+    assert call(5, 3, x=[xp[0], xp[1], None]) == _lib.NKV_EINVAL and "zm" in _lib.last_error()
+    assert call(6, 3) == _lib.NKV_EINVAL        # 216 points per element do not divide n_v
+    assert call(11, 3) == _lib.NKV_EINVAL
+    assert call(5, 3, nfld=0) == _lib.NKV_EINVAL
+    assert call(5, 3, nfld=2, us=n - 1) == _lib.NKV_EINVAL and "strides" in _lib.last_error()
+    assert call(5, 3, gs=n - 1) == _lib.NKV_EINVAL
+    assert call(5, 3, grad=None) == _lib.NKV_EINVAL
     assert lib.nkv_bf_sensitivity(ctx._Lp, u.data_ptr(), u.data_ptr(), u.data_ptr(), None, u.data_ptr(),
                                   u.data_ptr(), 3, ctx.stream) == _lib.NKV_EINVAL
+
+
+def test_gradm1_several_fields_one_launch(gpu):
+    """nfld fields at a stride in one launch equal one launch per field, bit for bit."""
+    ne = (3, 2, 2)
+    lay = NekLayout(ldim=3, lx1=6, lx2=4, nelgv=12)
+    ctx = _ctx(lay)
+    co = deformed_box(lay, ne)
+    op = Gradm1(ctx, co)
+    n, stride = lay.n_v, lay.n_v + 78   # every field 16-byte aligned, as every pointer of the ABI
+    rng = np.random.default_rng(2)
+    u = torch.as_tensor(rng.standard_normal(3 * stride)).to(ctx.device)
+    many = torch.full((3 * 3, n + 6), np.nan, dtype=torch.float64, device=ctx.device)
+    op(u.data_ptr(), many.data_ptr(), nfld=3, u_stride=stride, g_stride=n + 6)
+    for f in range(3):
+        one = torch.empty((3, n), dtype=torch.float64, device=ctx.device)
+        op(u.data_ptr() + 8 * f * stride, one.data_ptr())
+        assert torch.equal(one, many[3 * f: 3 * f + 3, :n])
+    assert torch.all(torch.isnan(many[:, n:]))
 
 
 @pytest.mark.parametrize("ldim", [2, 3])
@@ -209,17 +232,18 @@ def test_bf_sensitivity_config5_mesh(gpu, tmp_path):
         vecs.append(ctx.vector().from_packed(host))
     op = Gradm1(ctx, co)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    tmp = [torch.empty(vl.n_v, dtype=torch.float64, device=ctx.device) for _ in range(3)]
-    op(vecs[0].ptr, [t.data_ptr() for t in tmp])
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(5):
-        op(vecs[0].ptr, [t.data_ptr() for t in tmp])
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / 5
-    gbs = 7 * 8 * vl.n_v / (ms * 1e-3) / 1e9     # x, y, z, u read; ux, uy, uz written
-    print(f"gradm1 lx1=8 E={nel}: {ms:.3f} ms per field, {gbs:.0f} GB/s of algorithmic traffic")
+    tmp = torch.empty(9 * vl.sv, dtype=torch.float64, device=ctx.device)
+    for nfld, bytes_per_pt in ((1, 7), (3, 15)):   # x, y, z + nfld fields read, 3 nfld gradients written
+        op(vecs[0].ptr, tmp.data_ptr(), nfld=nfld, u_stride=vl.sv, g_stride=vl.sv)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(5):
+            op(vecs[0].ptr, tmp.data_ptr(), nfld=nfld, u_stride=vl.sv, g_stride=vl.sv)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 5
+        gbs = bytes_per_pt * 8 * vl.n_v / (ms * 1e-3) / 1e9
+        print(f"gradm1 lx1=8 E={nel} nfld={nfld}: {ms:.3f} ms per launch, {gbs:.0f} GB/s of algorithmic traffic")
     out, grad = bf_sensitivity_fields(ctx, *vecs, op, face_average=None)
     torch.cuda.synchronize()
     G = grad.view(4, 3, 3, vl.sv)[..., : vl.n_v]
