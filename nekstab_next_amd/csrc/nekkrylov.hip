@@ -1981,7 +1981,7 @@ __global__ __launch_bounds__((gradm1_threads<LDIM, NX>())) void k_gradm1(int64_t
     for (int t = tid; t < NX * NX; t += blockDim.x) D[t] = Dg[t];
     const int le = tid / pts, r = tid - le * pts;
     const int i = r % NX, j = (r / NX) % NX, k = LDIM == 3 ? r / (NX * NX) : 0;
-    const int base = le * pts;
+    const int base = (tid < nt ? le : 0) * pts;   // lanes past the last whole element read element 0
     const int ri = base + j * sj + k * sk;   // line along r through (., j, k)
     const int si = base + i + k * sk;        // line along s through (i, ., k)
     const int ti = base + i + j * sj;        // line along t through (i, j, .)
