@@ -59,7 +59,9 @@ def device_identity(device=None) -> dict:
     idx = torch.cuda.current_device() if device is None else torch.device(device).index
     pr = torch.cuda.get_device_properties(idx)
     pci = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
-    return {"device": int(idx), "name": pr.name, "pci": pci, "uuid": str(getattr(pr, "uuid", "")),
+    # the marketing name comes from libdrm's amdgpu.ids, absent on some hosts: fall back to the ISA name
+    name = pr.name or str(getattr(pr, "gcnArchName", "")).split(":")[0]
+    return {"device": int(idx), "name": name, "pci": pci, "uuid": str(getattr(pr, "uuid", "")),
             "host": os.uname().nodename}
 
 
