@@ -127,6 +127,7 @@ VARIANTS = {
     # rotation operands, few-column rotation at 9..16 columns) was retired in round 3; its logs stay
     # under profiles/r02*_tune_*.
     "fuse_fw_lds": {"patch": "fuse_fw_lds"},   # fused CGS2 pass: one wave loads f and w per tile
+    "fuse_rows2": {"patch": "fuse_rows2"},     # fused CGS2 pass: two row pairs per lane, half the barriers per byte
     "d2_prefetch": {"patch": "d2_prefetch"},   # two-vector multi-dot: next column group loaded during the reduction
     "dcnorm_units": {"patch": "dcnorm_units"},   # fused-norm dual update: row-tile units at every size (before r03ai)
     "d2_prefetch_ps8": {"patch": "d2_prefetch", "NKV_SMALL_TILES": 0},
