@@ -36,6 +36,7 @@ def test_bench_json_contract(gpu):
     assert cb["value_reference_executed_gbs"] > cb["value"]
     assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
     assert len(d["devices"]) == 1 and d["devices"][0]["pci"] and d["distinct_devices"] is True
+    assert d["devices"][0]["name"]   # the marketing name, or the ISA name where libdrm has none
     ks = d["krylov_schur_leg"]
     assert ks["schur_cnt"] >= 1 and ks["converged"] >= 4 and ks["ritz_rel_err_vs_exact"] < 1e-10
     assert d["ritz_top8_rel_err"] < 1e-10
