@@ -33,10 +33,13 @@ def log_transform(x: complex) -> complex:
 
 
 def write_hes(path: str, H: np.ndarray, k: int) -> None:
-    with open(path, "w") as fh:
+    d, b = os.path.split(path)
+    tmp = os.path.join(d, f".{b}.part{os.getpid()}")   # renamed into place: never read half written
+    with open(tmp, "w") as fh:
         for i in range(k + 1):
             for j in range(k):
                 fh.write(f"{H[i, j]: .17E}\n")
+    os.replace(tmp, path)
 
 
 def _list_directed_reals(text: str, count: int, path: str) -> np.ndarray:
@@ -100,25 +103,62 @@ class ArnoldiCheckpoint:
 
     def __call__(self, mstep: int, Q: Basis, Hd: HessenbergDev) -> None:
         k = mstep
-        if k == 1:  # Q(1) is written when the factorisation starts (eigensolvers.f90:235-236)
-            self.write_vector(Q[0], 1, time=0.0)
-        self.write_vector(Q[k], k + 1, time=float(k))   # whereyouwant("KRY", k+1)
-        if self.ctx.comm.rank != 0:
-            return
-        H = Hd.download()
-        if self.spectra:
-            vals, vecs = lapack.eig(H[:k, :k])
-            res = np.abs(H[k, k - 1] * vecs[k - 1, :])
-            write_spectra(self.dir, self.evop, k, vals, res, self.period)
-        write_hes(os.path.join(self.dir, f"HES{self.session}{k:04d}"), H, k)
+        # outpost2 is collective: on return every rank's KRY file and rank 0's HES are in place
+        with fld.collective_output(self.ctx.comm):
+            if k == 1:  # Q(1) is written when the factorisation starts (eigensolvers.f90:235-236)
+                self.write_vector(Q[0], 1, time=0.0)
+            self.write_vector(Q[k], k + 1, time=float(k))   # whereyouwant("KRY", k+1)
+            if self.ctx.comm.rank == 0:
+                H = Hd.download()
+                if self.spectra:
+                    vals, vecs = lapack.eig(H[:k, :k])
+                    res = np.abs(H[k, k - 1] * vecs[k - 1, :])
+                    write_spectra(self.dir, self.evop, k, vals, res, self.period)
+                write_hes(os.path.join(self.dir, f"HES{self.session}{k:04d}"), H, k)
+
+
+def read_restart_hes(comm, directory: str, session: str, mstart: int, k_dim: int, device=None) -> np.ndarray:
+    """H for a restart at ``mstart``: rank 0 parses ``HES<session><mstart>`` and broadcasts the
+    (k_dim+1) x k_dim matrix to every rank (eigensolvers.f90:244-266: ``if (nid == 0)`` read, then
+    ``bcast(H, (k_dim+1)*k_dim*wdsize)``).  A parse error on rank 0 is broadcast too (a NaN flag),
+    so every rank raises instead of waiting at the broadcast."""
+    import torch
+
+    H = np.zeros((k_dim + 1, k_dim), order="F")
+    err = None
+    if comm.rank == 0:
+        try:
+            H = read_hes(os.path.join(directory, f"HES{session}{mstart:04d}"), mstart, k_dim)
+        except (OSError, ValueError) as e:
+            err = e
+    if comm.world > 1:
+        t = torch.zeros(H.size + 1, dtype=torch.float64, device=device)
+        if comm.rank == 0:
+            t[:-1] = torch.as_tensor(H.ravel(order="F"))
+            t[-1] = 1.0 if err is None else float("nan")
+        comm.broadcast_(t, src=0)
+        host = t.cpu().numpy()
+        if not np.isfinite(host[-1]):
+            raise err if err is not None else ValueError(f"rank 0 could not read HES{session}{mstart:04d}")
+        H = np.asfortranarray(host[:-1].reshape((k_dim + 1, k_dim), order="F"))
+    elif err is not None:
+        raise err
+    return H
+
+
+def restart_vectors(lay, directory: str, session: str, mstart: int, comm=None):
+    """KRY 1..mstart+1 of this rank's shard, one padded host vector at a time (``load_files``,
+    IO.f90:12-73, after ``mstart = mstart + 1``): each rank opens only the files holding its own
+    elements (``fld.read_fld_set`` with the layout), so host memory stays one vector."""
+    for i in range(1, mstart + 2):
+        yield fld.vector_from_fld(lay, fld.read_fld_set(directory, "KRY", session, i, lay=lay, comm=comm))
 
 
 def load_restart(ctx: NekContext, directory: str, session: str, mstart: int, k_dim: int):
-    """(Q, H) for ``krylov_schur(..., Q=Q, start=(mstart, H))``: Q[0:mstart+1] = KRY 1..mstart+1."""
-    lay = ctx.layout
-    H = read_hes(os.path.join(directory, f"HES{session}{mstart:04d}"), mstart, k_dim)
+    """(Q, H) for ``krylov_schur(..., Q=Q, start=(mstart, H))``: Q[0:mstart+1] = KRY 1..mstart+1,
+    H read on rank 0 and broadcast."""
+    H = read_restart_hes(ctx.comm, directory, session, mstart, k_dim, device=ctx.device)
     Q = ctx.basis(k_dim + 1)
-    for i in range(1, mstart + 2):
-        files = fld.read_fld_set(directory, "KRY", session, i)
-        Q[i - 1].from_packed(fld.vector_from_fld(lay, files))
+    for i, v in enumerate(restart_vectors(ctx.layout, directory, session, mstart, ctx.comm)):
+        Q[i].from_packed(v)
     return Q, H

@@ -106,6 +106,22 @@ class Comm:
         dist.all_gather_object(out, me, group=self.group)
         return out
 
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        """In-place broadcast from ``src`` (the reference's ``bcast``, e.g. the restart H at
+        eigensolvers.f90:266)."""
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def bcast_object(self, obj, src: int = 0):
+        """A picklable host object from ``src`` to every rank (setup-only messages: a file
+        header, an error to raise everywhere)."""
+        if self.world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.group)
+        return box[0]
+
     def barrier(self) -> None:
         if self.world > 1:
             dist.barrier(group=self.group)

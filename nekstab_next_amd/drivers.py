@@ -57,11 +57,12 @@ def linear_stability_analysis(ctx: NekContext, A: LinearOperator, seed: NekVecto
     if outdir:
         os.makedirs(outdir, exist_ok=True)
         v = ctx.vector()
-        for i in range(min(cfg.maxmodes, cfg.k_dim)):
-            get_vec(v, X, vecs[:, i].real, cfg.k_dim)
-            _export(ctx, v, outdir, f"{evop}Re", session, i + 1, float(i + 1))
-            get_vec(v, X, vecs[:, i].imag, cfg.k_dim)
-            _export(ctx, v, outdir, f"{evop}Im", session, i + 1, float(i + 1))
+        with fld.collective_output(ctx.comm):   # outpost2 is collective: the sets are whole on return
+            for i in range(min(cfg.maxmodes, cfg.k_dim)):
+                get_vec(v, X, vecs[:, i].real, cfg.k_dim)
+                _export(ctx, v, outdir, f"{evop}Re", session, i + 1, float(i + 1))
+                get_vec(v, X, vecs[:, i].imag, cfg.k_dim)
+                _export(ctx, v, outdir, f"{evop}Im", session, i + 1, float(i + 1))
     return dict(eigvals=vals, eigvals_ns=vals_ns, residuals=res, eigvecs=vecs, info=info, X=X)
 
 
@@ -80,11 +81,12 @@ def transient_growth_analysis(ctx: NekContext, A: LinearOperator, seed: NekVecto
     if outdir:
         os.makedirs(outdir, exist_ok=True)
         v = ctx.vector()
-        for i in range(min(maxmodes, nev)):
-            get_vec(v, U, r.uvecs[:, i], k_dim)
-            _export(ctx, v, outdir, "pU", session, i + 1, float(i + 1))
-            get_vec(v, V, r.vvecs[:, i], k_dim)
-            _export(ctx, v, outdir, "pV", session, i + 1, float(i + 1))
+        with fld.collective_output(ctx.comm):
+            for i in range(min(maxmodes, nev)):
+                get_vec(v, U, r.uvecs[:, i], k_dim)
+                _export(ctx, v, outdir, "pU", session, i + 1, float(i + 1))
+                get_vec(v, V, r.vvecs[:, i], k_dim)
+                _export(ctx, v, outdir, "pV", session, i + 1, float(i + 1))
     return dict(gain=gain, sigma=r.sigma, residuals=r.residuals, info=r.info, U=U, V=V, svd=r)
 
 

@@ -17,9 +17,22 @@ eigensolvers.f90:170-180) and writes Krylov vectors / eigenmodes with ``outpost2
 
 Multi-rank: each rank writes its element range as file ``fid = rank`` with ``nfileo = world``
 (Nek5000's multi-file naming ``<prefix><session><fid>.f<NNNNN>``).
+
+Collective semantics.  Nek5000's ``outpost2`` and ``load_fld`` are collective: every rank has
+finished writing a set before any rank reads from it (the reference relies on it at
+eigensolvers.f90:607-615 -> sensitivity.f90:40-60, and on restart, IO.f90:12-73).  Here:
+
+* :func:`write_fld` writes to a temporary name in the same directory and ``os.replace``-s it into
+  place, so a reader never sees a partly written file;
+* every product writer of a per-rank set ends in :func:`collective_output` (a barrier over the
+  ranks' communicator once this rank's files are in place);
+* :func:`read_fld_set` raises when a member of a set is missing (never a partial set), and with a
+  layout it opens only the files holding this rank's elements: with a set written at the same
+  world size, rank r opens fid r and nothing else.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass, field
 
@@ -114,22 +127,40 @@ def _groups(rdcode: str):
     return out
 
 
+def _parse_header(raw, path: str):
+    """(wdsize, nx, ny, nz, nel, nelgt, time, istep, fid0, nfileo, rdcode, byte order, emap)."""
+    if len(raw) < 136:
+        raise ValueError(f"{path}: {len(raw)} bytes, shorter than a #std header")
+    tok = bytes(raw[:132]).decode("ascii", errors="replace").split()
+    if not tok or tok[0] != "#std":
+        raise ValueError(f"{path}: not a Nek5000 #std field file")
+    wdsize, nx, ny, nz, nel, nelgt = (int(t) for t in tok[1:7])
+    time, istep, fid0, nfileo = float(tok[7]), int(tok[8]), int(tok[9]), int(tok[10])
+    tag = np.frombuffer(raw, "<f4", count=1, offset=132)[0]
+    order = "<" if abs(tag - ENDIAN_TAG) < 1e-5 else ">"
+    if len(raw) < 136 + 4 * nel:
+        raise ValueError(f"{path}: truncated element map ({nel} elements)")
+    emap = np.frombuffer(raw, order + "i4", count=nel, offset=136).copy()
+    return wdsize, nx, ny, nz, nel, nelgt, time, istep, fid0, nfileo, tok[11], order, emap
+
+
+def read_fld_header(path: str) -> FldFile:
+    """Header and element map only (no field data): 136 + 4 nel bytes."""
+    with open(path, "rb") as fh:
+        head = fh.read(136)
+        nel = int(bytes(head[:132]).decode("ascii", errors="replace").split()[5]) if len(head) >= 132 else 0
+        raw = head + fh.read(4 * max(nel, 0))
+    wdsize, nx, ny, nz, nel, nelgt, time, istep, fid0, nfileo, rdcode, _, emap = _parse_header(raw, path)
+    return FldFile(nx, ny, nz, nelgt, time, istep, fid0, nfileo, rdcode, emap, {}, wdsize)
+
+
 def read_fld(path: str) -> FldFile:
     # one read into a mutable buffer; the fields are views of it (no payload copies)
     raw = bytearray(os.path.getsize(path))
     with open(path, "rb") as fh:
         if fh.readinto(raw) != len(raw):
             raise ValueError(f"{path}: short read")
-    hdr = bytes(raw[:132]).decode("ascii", errors="replace")
-    tok = hdr.split()
-    if tok[0] != "#std":
-        raise ValueError(f"{path}: not a Nek5000 #std field file")
-    wdsize, nx, ny, nz, nel, nelgt = (int(t) for t in tok[1:7])
-    time, istep, fid0, nfileo = float(tok[7]), int(tok[8]), int(tok[9]), int(tok[10])
-    rdcode = tok[11]
-    tag = np.frombuffer(raw, "<f4", count=1, offset=132)[0]
-    order = "<" if abs(tag - ENDIAN_TAG) < 1e-5 else ">"
-    emap = np.frombuffer(raw, order + "i4", count=nel, offset=136).copy()
+    wdsize, nx, ny, nz, nel, nelgt, time, istep, fid0, nfileo, rdcode, order, emap = _parse_header(raw, path)
     fdt = np.dtype(order + ("f8" if wdsize == 8 else "f4"))
     data = np.frombuffer(raw, fdt, offset=136 + 4 * nel)
     if data.dtype != np.dtype(np.float64):   # byte-swapped or single precision: one converted copy
@@ -170,9 +201,32 @@ def write_fld(path: str, f: FldFile) -> None:
             parts.append(np.ascontiguousarray(blk, "<f8"))
         else:
             parts.append(np.ascontiguousarray(f.fields[{"P": "pr", "T": "t"}.get(g, g.lower())], "<f8"))
-    with open(path, "wb") as fh:
-        for p in parts:
-            fh.write(memoryview(p).cast("B") if isinstance(p, np.ndarray) else p)
+    # written under a temporary name in the same directory, then renamed into place (atomic on
+    # POSIX): a reader on another rank sees either no file or the whole file
+    d, b = os.path.split(path)
+    tmp = os.path.join(d, f".{b}.part{os.getpid()}")
+    try:
+        with open(tmp, "wb") as fh:
+            for p in parts:
+                fh.write(memoryview(p).cast("B") if isinstance(p, np.ndarray) else p)
+        os.replace(tmp, path)
+    except BaseException:
+        with contextlib.suppress(OSError):
+            os.remove(tmp)
+        raise
+
+
+@contextlib.contextmanager
+def collective_output(comm, barrier: bool = True):
+    """The collective end of a per-rank ``outpost2``: the body writes this rank's files (and rank
+    0's text files); on a normal exit every rank waits at a barrier until all ranks' files are in
+    place, so a read that follows on any rank finds the whole set (Nek5000's outpost2 / load_fld
+    are collective, eigensolvers.f90:607-615, sensitivity.f90:40-60).  An exception skips the
+    barrier (the peers then fail at their next collective, bounded by ``comm``'s timeout).
+    ``barrier=False`` exists only for the test that shows the race without it."""
+    yield
+    if barrier and comm is not None:
+        comm.barrier()
 
 
 def fld_name(prefix: str, session: str, fid: int, num: int) -> str:
@@ -239,19 +293,76 @@ def fld_from_vector(lay: NekLayout, vec: np.ndarray, time: float = 0.0, istep: i
     return f
 
 
-def read_fld_set(directory: str, prefix: str, session: str, num: int) -> list:
-    """All files of a (possibly multi-file) output number."""
-    out = []
-    fid = 0
-    while True:
-        p = os.path.join(directory, fld_name(prefix, session, fid, num))
-        if not os.path.exists(p):
-            break
-        f = read_fld(p)
-        out.append(f)
-        fid += 1
-        if fid >= f.nfileo:
-            break
-    if not out:
-        raise FileNotFoundError(os.path.join(directory, fld_name(prefix, session, 0, num)))
-    return out
+def _block(fid: int, nfileo: int, nelgt: int) -> tuple[int, int]:
+    """Elements [e0, e1) (0-based) of file ``fid`` of a set written by ``nfileo`` ranks with
+    Nek5000's element-contiguous distribution (layout.NekLayout.elem_range)."""
+    return (fid * nelgt) // nfileo, ((fid + 1) * nelgt) // nfileo
+
+
+def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLayout | None = None,
+                 comm=None) -> list:
+    """The files of a (possibly multi-file) output number, as Nek5000's ``load_fld`` reads them.
+
+    Without ``lay``: every file of the set.  With ``lay``: only the files holding elements of
+    ``lay.elem_range()`` (this rank's shard).  The set is defined by the header of fid 0 (a
+    set's first member is always rewritten, so leftover higher fids of an older, larger set are
+    ignored): with ``comm`` at world > 1, rank 0 reads that header and broadcasts (nfileo,
+    nelgt), so with a set written at the same world size rank r opens fid r and nothing else.  The
+    files a rank needs are predicted from the element-contiguous distribution of an
+    nfileo-file set; each one's element map is checked against the prediction, and only a set
+    written with another distribution (a foreign writer) falls back to reading every header.
+
+    Raises FileNotFoundError when fid 0 or any member fid < nfileo is missing (on every rank), and
+    ValueError when the files read do not cover the shard's elements — never a partial vector."""
+    def path(fid):
+        return os.path.join(directory, fld_name(prefix, session, fid, num))
+
+    def set_header():
+        if not os.path.exists(path(0)):
+            return FileNotFoundError(path(0))
+        try:
+            h = read_fld_header(path(0))
+        except (OSError, ValueError) as e:
+            return e
+        if h.nfileo < 1:
+            return ValueError(f"{path(0)}: nfileo={h.nfileo}")
+        return h.nfileo, h.nelgt
+
+    if comm is not None and comm.world > 1:
+        hdr = comm.bcast_object(set_header() if comm.rank == 0 else None, src=0)
+    else:
+        hdr = set_header()
+    if isinstance(hdr, BaseException):
+        raise hdr
+    n, nelgt = hdr
+    missing = [i for i in range(n) if not os.path.exists(path(i))]
+    if missing:
+        raise FileNotFoundError(f"{path(missing[0])} (set of {n} files, missing fids {missing})")
+    if lay is None:
+        return [read_fld(path(i)) for i in range(n)]
+
+    e0, e1 = lay.elem_range()
+    E = lay.nelgv
+    if nelgt != E:
+        raise ValueError(f"{path(0)}: nelgt={nelgt}, the layout has {E} elements")
+
+    def holds_ours(emap):
+        g = emap.astype(np.int64) - 1
+        return bool(np.any((g >= e0) & (g < e1)))
+
+    want = [i for i in range(n) if _block(i, n, E)[0] < e1 and _block(i, n, E)[1] > e0]
+    out = {i: read_fld(path(i)) for i in want}
+    if not all(np.array_equal(out[i].emap, np.arange(*_block(i, n, E)) + 1) for i in want):
+        # another element distribution: every header decides, then the files holding our elements
+        for i in range(n):
+            if i not in out and holds_ours(read_fld_header(path(i)).emap):
+                out[i] = read_fld(path(i))
+    files = [out[i] for i in sorted(out) if holds_ours(out[i].emap)]
+    covered = np.zeros(e1 - e0, dtype=bool)
+    for f in files:
+        g = f.emap.astype(np.int64) - 1
+        covered[g[(g >= e0) & (g < e1)] - e0] = True
+    if not covered.all():
+        raise ValueError(f"{prefix}{session}*.f{num:05d}: {int((~covered).sum())} of this rank's "
+                         f"{e1 - e0} elements are in no file of the set")
+    return files

@@ -135,9 +135,7 @@ def load_seed(ctx: NekContext, directory: str, session: str = "nek", transpose: 
     from . import fld
 
     prefix = "aRe" if transpose else "dRe"
-    files = fld.read_fld_set(directory, prefix, session, 1)
-    if not files:
-        raise FileNotFoundError(f"{fld.fld_name(prefix, session, 0, 1)} not found in {directory}")
+    files = fld.read_fld_set(directory, prefix, session, 1, lay=ctx.layout, comm=ctx.comm)
     return ctx.vector().from_packed(fld.vector_from_fld(ctx.layout, files))
 
 
@@ -267,9 +265,10 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
 
 
 def ritz_vector(ctx: NekContext, Q: Basis, vecs: np.ndarray, i: int, out_re: NekVector, out_im: NekVector,
-                k: int | None = None) -> tuple[float, float]:
+                k: int | None = None, normalize: bool = True) -> tuple[float, float]:
     """Eigenmode i from the basis: fp = Q(:,1:k) vecs(:,i) (complex, as two real combinations),
-    normalised so that ||Re||^2 + ||Im||^2 = 1 (outpost_ks, eigensolvers.f90:565-585, 603-613).
+    normalised so that ||Re||^2 + ||Im||^2 = 1 (outpost_ks, eigensolvers.f90:565-585, 603-613;
+    ``normalize=False`` leaves fp as assembled, the vector ``norm_grad`` sees, :587-588).
     Returns (||Re||, ||Im||) before normalisation."""
     from .vector import combine
 
@@ -280,9 +279,10 @@ def ritz_vector(ctx: NekContext, Q: Basis, vecs: np.ndarray, i: int, out_re: Nek
     combine(out_im, Q, yi, k, with_time=False)
     a_r = float(np.sqrt(ctx.dot(out_re, out_re, time=False)))
     a_i = float(np.sqrt(ctx.dot(out_im, out_im, time=False)))
-    beta = 1.0 / np.sqrt(a_r ** 2 + a_i ** 2)
-    out_re.scal(beta)
-    out_im.scal(beta)
+    if normalize:
+        beta = 1.0 / np.sqrt(a_r ** 2 + a_i ** 2)
+        out_re.scal(beta)
+        out_im.scal(beta)
     return a_r, a_i
 
 
@@ -307,16 +307,22 @@ def orthonormality_report(ctx: NekContext, Q: Basis, k: int) -> np.ndarray:
 
 def outpost_ks(ctx: NekContext, res: KrylovSchurResult, outdir: str, evop: str = "d", period: float = 1.0,
                maxmodes: int = 20, session: str = "nek", k: int | None = None,
-               orthonormality: bool = True) -> dict:
+               orthonormality: bool = True, coords: dict | None = None, grad_tol: float = 1.1) -> dict:
     """The end of the in-tree ``krylov_schur`` (eigensolvers.f90:335-349) and ``outpost_ks``
     (:472-640): ``orthonormality.dat``; ``Spectre_H<evop>.dat`` (re, im, residual of every Ritz
     value, 3E15.7) and ``Spectre_NS<evop>.dat`` (log-transformed, divided by the sampling period
     dt*nsteps); for the first ``converged`` modes, up to ``maxmodes``: the eigenmode
     Q(:,1:k) vecs(:,i), normalised so ||Re||^2 + ||Im||^2 = 1, written as ``<evop>Re`` /
     ``<evop>Im`` field files numbered 1.. (time = output number), and its log-transformed value
-    appended to ``Spectre_NS<evop>_conv.dat`` (2E15.7).  The reference skips modes whose
-    gradient norm exceeds 1.1 (Nek5000 ``norm_grad``, a spectral-element derivative): that filter
-    needs the mesh and is not applied here.  Returns the written mode indices."""
+    appended to ``Spectre_NS<evop>_conv.dat`` (2E15.7).
+
+    Spurious-mode filter (:587-595): with ``coords`` (this rank's GLL coordinates {"x","y"[,"z"]},
+    e.g. ``seeds.coords_from_fld``) the squared gradient norms of Re and Im of the assembled,
+    not yet normalised mode are taken (``norm_grad``, utils.f90:446-486, on the device:
+    :class:`~.sensitivity.NormGrad`), and a mode with either above ``grad_tol`` (1.1) is skipped:
+    not written, not in ``_conv.dat``, and the following modes take its output number (the
+    reference's ``outp`` counter).  Without coords no mode is filtered (the mesh is the case's).
+    Returns the written mode indices, the skipped ones and every (Re, Im) gradient norm."""
     from . import fld
     from .checkpoint import log_transform
 
@@ -339,21 +345,36 @@ def outpost_ks(ctx: NekContext, res: KrylovSchurResult, outdir: str, evop: str =
                 f1.write(f"{v.real:15.7E}{v.imag:15.7E}{r:15.7E}\n")
                 lt = log_transform(v)
                 f2.write(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}{r:15.7E}\n")
-    written = []
+    written, skipped, grad_norms = [], [], {}
     re_v, im_v = ctx.vector(), ctx.vector()
     conv_lines = []
-    for i in range(res.converged):
-        if len(written) >= maxmodes:
-            break
-        ritz_vector(ctx, res.Q, res.vecs, i, re_v, im_v, k=k)
-        num = len(written) + 1
-        for vec, name in ((re_v, f"{evop}Re"), (im_v, f"{evop}Im")):
-            f = fld.fld_from_vector(lay, vec.to_packed(), time=float(num), istep=num)
-            fld.write_fld(os.path.join(outdir, fld.fld_name(name, session, lay.rank, num)), f)
-        lt = log_transform(res.vals[i])
-        conv_lines.append(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}\n")
-        written.append(i)
-    if ctx.comm.rank == 0:
-        with open(os.path.join(outdir, f"Spectre_NS{evop}_conv.dat"), "w") as fh:
-            fh.writelines(conv_lines)
-    return dict(modes=written)
+    ng = None
+    if coords is not None:
+        from .sensitivity import NormGrad
+
+        ng = NormGrad(ctx, coords)
+    with fld.collective_output(ctx.comm):   # outpost2 is collective: the set is whole on return
+        for i in range(res.converged):
+            if len(written) >= maxmodes:
+                break
+            a_r, a_i = ritz_vector(ctx, res.Q, res.vecs, i, re_v, im_v, k=k, normalize=ng is None)
+            if ng is not None:
+                g_re, g_im = ng(re_v), ng(im_v)   # on fp before nopcmult (:587-588)
+                grad_norms[i] = (g_re, g_im)
+                if g_re > grad_tol or g_im > grad_tol:
+                    skipped.append(i)   # "Skipping spurious (non-physical) eigenvector" (:592-595)
+                    continue
+                beta = 1.0 / np.sqrt(a_r ** 2 + a_i ** 2)
+                re_v.scal(beta)
+                im_v.scal(beta)
+            num = len(written) + 1
+            for vec, name in ((re_v, f"{evop}Re"), (im_v, f"{evop}Im")):
+                f = fld.fld_from_vector(lay, vec.to_packed(), time=float(num), istep=num)
+                fld.write_fld(os.path.join(outdir, fld.fld_name(name, session, lay.rank, num)), f)
+            lt = log_transform(res.vals[i])
+            conv_lines.append(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}\n")
+            written.append(i)
+        if ctx.comm.rank == 0:
+            with open(os.path.join(outdir, f"Spectre_NS{evop}_conv.dat"), "w") as fh:
+                fh.writelines(conv_lines)
+    return dict(modes=written, skipped=skipped, grad_norms=grad_norms)

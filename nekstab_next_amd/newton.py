@@ -71,5 +71,6 @@ def newton_krylov(ctx: NekContext, nonlinear, linearized, q: NekVector, tol: flo
 
         lay = ctx.layout
         res.path = os.path.join(outdir, fld.fld_name("BF_", session, lay.rank, 1))
-        fld.write_fld(res.path, fld.fld_from_vector(lay, q.to_packed(), time=q.time, istep=res.iterations))
+        with fld.collective_output(ctx.comm):
+            fld.write_fld(res.path, fld.fld_from_vector(lay, q.to_packed(), time=q.time, istep=res.iterations))
     return res

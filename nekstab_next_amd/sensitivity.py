@@ -98,9 +98,7 @@ def _load_modes(ctx: NekContext, directory: str, session: str, d_num: int, a_num
         raise ValueError(f"{who} works on a velocity-only context (sensitivity.velocity_layout)")
     vecs, last = [], None
     for prefix, num in (("dRe", d_num), ("dIm", d_num), ("aRe", a_num), ("aIm", a_num)):
-        files = fld.read_fld_set(directory, prefix, session, num)
-        if not files:
-            raise FileNotFoundError(f"{fld.fld_name(prefix, session, 0, num)} not found in {directory}")
+        files = fld.read_fld_set(directory, prefix, session, num, lay=lay, comm=ctx.comm)   # this rank's elements only
         last = files[0]
         v = ctx.vector()
         v.from_packed(fld.vector_from_fld(lay, files))
@@ -186,6 +184,44 @@ class Gradm1:
                       int(u_stride), grad_ptr, int(lay.n_v if g_stride is None else g_stride), self.ctx.stream)
 
 
+class NormGrad:
+    """Nek5000-side ``norm_grad`` (core/utils.f90:446-486) on the device: ``gradm1`` of vx, vy[, vz]
+    of a state vector (one ``nkv_gradm1`` launch for the ldim components), then the sum of the
+    ``glsc3(g, bm1s, g)`` of every gradient component — dudx, dudy, dvdx, dvdy, and in 3-D also
+    dudz, dvdz, dwdx, dwdy, dwdz, i.e. all ldim x ldim of them (:476-485) — as ONE weighted dot over
+    the ldim^2 gradient segments plus one all-reduce (glsc3's per-term all-reduces summed in
+    another order: the same value to rounding).  No ``dsavg`` (commented out in the reference,
+    :470-472).  The squared norm, no square root, as the reference compares it (with 1.1,
+    eigensolvers.f90:592).  ``coords``: this rank's GLL coordinates."""
+
+    def __init__(self, ctx: NekContext, coords: dict):
+        from .layout import _roundup
+
+        lay = ctx.layout
+        self.ctx = ctx
+        self.grad_op = coords if isinstance(coords, Gradm1) else Gradm1(ctx, coords)
+        nf = lay.ldim * lay.ldim
+        self.L = lay.c_struct()
+        self.L.n_wf = nf
+        self.L.n_p = 0
+        self.L.sp = 0
+        self.L.ld = _roundup(nf * lay.sv + 1, 4096)
+        self.grad = torch.zeros(self.L.ld, dtype=torch.float64, device=ctx.device)
+        self.out = torch.zeros(1, dtype=torch.float64, device=ctx.device)
+
+    def __call__(self, v: NekVector) -> float:
+        ctx, lay = self.ctx, self.ctx.layout
+        gp = self.grad.data_ptr()
+        self.grad_op(v.ptr, gp, nfld=lay.ldim, u_stride=lay.sv, g_stride=lay.sv)
+        _lib.check(ctx.lib.nkv_dot(ctypes.byref(self.L), ctx.w.data_ptr(), gp, gp, self.out.data_ptr(),
+                                   ctx.ws.data_ptr(), 0, ctx.stream), "nkv_dot(norm_grad)")
+        ctx.comm.allreduce_(self.out)
+        val = float(self.out.item())
+        if val != val:
+            ctx.check_nan()
+        return val
+
+
 BF_OUTPUTS = ("tr_", "ti_", "pr_", "pi_", "sr_", "si_")
 
 
@@ -237,15 +273,16 @@ def bf_sensitivity(ctx: NekContext, directory: str, coords: dict, session: str =
     dst = outdir or directory
     os.makedirs(dst, exist_ok=True)
     result, paths = {}, []
-    for t, prefix in enumerate(BF_OUTPUTS):
-        f = _out_file(lay, last, coords if write_coords else None)
-        for c, nm in enumerate(("vx", "vy", "vz")[: lay.ldim]):
-            f.fields[nm] = host[t, c].reshape(lay.nelv, lay.pts_v)
-        f.rdcode += "U"
-        path = os.path.join(dst, fld.fld_name(prefix, session, lay.rank, 1))
-        fld.write_fld(path, f)
-        result[prefix.rstrip("_")] = [host[t, c].copy() for c in range(lay.ldim)]
-        paths.append(path)
+    with fld.collective_output(ctx.comm):   # outpost is collective: the sets are whole on return
+        for t, prefix in enumerate(BF_OUTPUTS):
+            f = _out_file(lay, last, coords if write_coords else None)
+            for c, nm in enumerate(("vx", "vy", "vz")[: lay.ldim]):
+                f.fields[nm] = host[t, c].reshape(lay.nelv, lay.pts_v)
+            f.rdcode += "U"
+            path = os.path.join(dst, fld.fld_name(prefix, session, lay.rank, 1))
+            fld.write_fld(path, f)
+            result[prefix.rstrip("_")] = [host[t, c].copy() for c in range(lay.ldim)]
+            paths.append(path)
     return dict(fields=result, inner_product=ip, paths=paths, vectors=(dRe, dIm, aRe, aIm))
 
 
@@ -276,9 +313,9 @@ def wave_maker(ctx: NekContext, directory: str, session: str = "nek", d_num: int
     out = outdir or directory
     os.makedirs(out, exist_ok=True)
     path = os.path.join(out, fld.fld_name("wm_", session, lay.rank, 1))
-    fld.write_fld(path, f)
+    with fld.collective_output(ctx.comm):
+        fld.write_fld(path, f)
     return dict(wavemaker=wm, inner_product=ip, path=path, vectors=(dRe, dIm, aRe, aIm))
-
 
 
 def ts_steady_force_sensitivity(ctx: NekContext, op, directory: str, session: str = "nek", part: str = "r",
@@ -303,9 +340,7 @@ def ts_steady_force_sensitivity(ctx: NekContext, op, directory: str, session: st
     if part not in ("r", "i"):
         raise ValueError("part must be 'r' (uparam(1) = 4.41) or 'i' (4.42)")
     lay = ctx.layout
-    files = fld.read_fld_set(directory, f"s{part}_", session, 1)
-    if not files:
-        raise FileNotFoundError(f"{fld.fld_name(f's{part}_', session, 0, 1)} not found in {directory}")
+    files = fld.read_fld_set(directory, f"s{part}_", session, 1, lay=lay, comm=ctx.comm)
     full = fld.vector_from_fld(lay, files)
     host = np.zeros(lay.ld)
     for c in range(lay.ldim):   # opcopy: the velocity components only
@@ -322,5 +357,6 @@ def ts_steady_force_sensitivity(ctx: NekContext, op, directory: str, session: st
     out = outdir or directory
     os.makedirs(out, exist_ok=True)
     path = os.path.join(out, fld.fld_name(f"fs{part}", session, lay.rank, 1))
-    fld.write_fld(path, fld.fld_from_vector(lay, sol.to_packed(), time=files[0].time, istep=1))
+    with fld.collective_output(ctx.comm):
+        fld.write_fld(path, fld.fld_from_vector(lay, sol.to_packed(), time=files[0].time, istep=1))
     return dict(solution=sol, alpha=alpha, info=info, path=path)

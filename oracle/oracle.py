@@ -640,6 +640,61 @@ def gradm1(lx1, ldim, coords, u):
             (jacmi * (ur * rz + us * sz + ut * tz)).ravel()]
 
 
+def norm_grad(lx1, ldim, coords, w, comps):
+    """``norm_grad`` (core/utils.f90:446-486): gradm1 of vx_, vy_[, vz_] (:466-468; no dsavg, it is
+    commented out at :470-472), then the glsc3 sums in the reference's order, left to right:
+    norma = (norma + |dudx|^2) + |dudy|^2 (:476), (norma + |dvdx|^2) + |dvdy|^2 (:477), and in 3-D
+    + |dudz|^2, + |dvdz|^2, + |dwdx|^2, + |dwdy|^2, + |dwdz|^2 (:480-484); |g|^2 = glsc3(g, bm1s, g)
+    on one rank.  ``comps``: the velocity components (reference point order)."""
+    g = [gradm1(lx1, ldim, coords, comps[c]) for c in range(ldim)]
+    sq = lambda a: glsc3_np(a, w, a)  # noqa: E731
+    norma = 0.0
+    norma = norma + sq(g[0][0]) + sq(g[0][1])
+    norma = norma + sq(g[1][0]) + sq(g[1][1])
+    if ldim == 3:
+        norma = norma + sq(g[0][2])
+        norma = norma + sq(g[1][2])
+        norma = norma + sq(g[2][0])
+        norma = norma + sq(g[2][1])
+        norma = norma + sq(g[2][2])
+    return norma
+
+
+def outpost_ks_modes(L: OLayout, w, Q, vecs, converged, k, lx1, coords, maxmodes=20, grad_tol=1.1):
+    """The mode loop of ``outpost_ks`` (eigensolvers.f90:555-615) with the spurious-mode filter:
+    for i = 1..converged (while outp < maxmodes) assemble fp = Q(:,1:k) vecs(:,i) (k_matmul order),
+    take norm_grad of its real and imaginary parts BEFORE the nopcmult (:587-588), skip the mode if
+    either exceeds 1.1 (:592-595), else outp = outp + 1 and the normalised Re/Im go out as file
+    number outp (:600-615).  Returns [(i, outp or None, g_re, g_im, re, im)] (re/im normalised,
+    None for skipped modes)."""
+    c = ctypes.byref(L.c)
+    Qk = np.ascontiguousarray(Q[:k])
+    nv, ldim = L.nv, L.ldim
+    out, outp = [], 0
+    for i in range(converged):
+        if outp >= maxmodes:
+            continue
+        re, im = L.zeros(), L.zeros()
+        lib().orc_k_matmul(c, re, Qk, np.ascontiguousarray(vecs[:k, i].real), k)
+        lib().orc_k_matmul(c, im, Qk, np.ascontiguousarray(vecs[:k, i].imag), k)
+        re[-1] = im[-1] = 0.0
+        nt = OLayout(L.nv, L.np, L.nwf, False, L.ldim)
+        ar = float(np.sqrt(k_dot(nt, w, re, re)))
+        ai = float(np.sqrt(k_dot(nt, w, im, im)))
+        beta = 1.0 / np.sqrt(ar ** 2 + ai ** 2)
+        g_re = norm_grad(lx1, ldim, coords, w, [re[d * nv:(d + 1) * nv] for d in range(ldim)])
+        g_im = norm_grad(lx1, ldim, coords, w, [im[d * nv:(d + 1) * nv] for d in range(ldim)])
+        if g_re > grad_tol or g_im > grad_tol:
+            out.append((i, None, g_re, g_im, None, None))
+            continue
+        outp += 1
+        lib().orc_k_cmult(c, re, beta)
+        lib().orc_k_cmult(c, im, beta)
+        re[-1] = im[-1] = 0.0
+        out.append((i, outp, g_re, g_im, re, im))
+    return out
+
+
 def bf_sensitivity_terms(ldim, d_re, d_im, a_re, a_im, g):
     """sensitivity.f90:202-235, 258-259 line by line.  d_re ... : lists of velocity components
     [vx, vy(, vz)]; g[(mode, comp, dir)] the dsavg'd gradients, mode in 'dRe','dIm','aRe','aIm',

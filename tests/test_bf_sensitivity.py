@@ -110,3 +110,23 @@ def test_bf_terms_tensor_form(ldim):
     pi = np.einsum("jn,ijn->in", modes["dRe"], aI) - np.einsum("jn,ijn->in", modes["dIm"], aR)
     for name, ref in (("tr", tr), ("ti", ti), ("pr", pr), ("pi", pi), ("sr", tr + pr), ("si", ti + pi)):
         np.testing.assert_allclose(np.array(t[name]), ref, rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("three", [False, True])
+def test_norm_grad_linear_fields_known_answer(three):
+    """oracle.norm_grad (utils.f90:446-486): linear velocity components have constant gradients,
+    so the squared gradient norm is sum(coefficients^2) * sum(bm1s) — on the reference's curved
+    cylinder mesh and on a deformed 3-D box."""
+    if three:
+        lay = NekLayout(ldim=3, lx1=5, lx2=3, nelgv=12)
+        co = deformed_box(lay, (3, 2, 2))
+    else:
+        lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=1996)
+        co = _cyl()
+    d = lay.ldim
+    rng = np.random.default_rng(2)
+    A = rng.uniform(-1, 1, (d, d))
+    comps = [sum(A[c, k] * co["xyz"[k]] for k in range(d)) + 0.5 for c in range(d)]
+    w = rng.uniform(0.5, 1.5, lay.n_v)
+    got = orc.norm_grad(lay.lx1, d, co, w, comps)
+    assert abs(got - np.sum(A * A) * w.sum()) <= 1e-9 * got
