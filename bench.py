@@ -28,7 +28,9 @@ that model divided by the same time is reported separately as ``effective_gbs_su
 work definition the CPU baseline is also reported in).  ``roofline`` is the dominant kernel family
 timed live with HIP events on the launch stream.  Outside the timed region: ``restart`` times one
 Krylov–Schur condensation of the final factorisation (H rescaled to unit spectral radius, see
-there), and ``krylov_schur_leg`` runs the config-3 operator through real Krylov–Schur restarts.
+there), ``krylov_schur_leg`` runs config 3's Krylov–Schur (k_dim=m, schur_tgt=4) and
+``krylov_schur_restart_leg`` the same with schur_tgt above the first factorisation's converged
+count, i.e. through a real m-column restart.
 """
 from __future__ import annotations
 
@@ -152,16 +154,19 @@ def host_threads() -> dict:
 
 # ---- CPU baseline ------------------------------------------------------------------------------
 
-def cpu_baseline(E_sample: int, m: int, threads: int, js, variant: str = "mgs2", n_full: int = N_HEADLINE):
-    """The reference algorithm timed on this host: MGS + full re-orthogonalisation with per-field
-    weighted dots (copy -> dot -> cmult -> sub2, krylov_decomposition.f90:152-186), restated in C
-    (oracle/nekstab_oracle.c, built -Ofast like the reference's bin/mks:53-55), on the config-3
-    layout at ``E_sample`` elements.  The basis Q[0:max(js)] is pre-built (hashed vectors; MGS2's
-    cost does not depend on the values), then single Arnoldi steps j in ``js`` are timed (matvec +
-    update_hessenberg_matrix on a fresh f).  The per-step time is linear in j, t(j) = a + b j
-    (least squares over ``js``), so a full m-step factorisation costs Σ_j t(j); it is reported at
-    the sample size and scaled by N to BASELINE's N=1e8 (seconds to solution).
-    ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2)."""
+def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_full: int = N_HEADLINE,
+                 fit_js=(1, 32, 64, 128)):
+    """The reference algorithm timed on this host: ONE complete m-step Arnoldi factorisation (after
+    one untimed warm-up step) — the synthetic matvec, then MGS + full re-orthogonalisation with
+    per-field weighted dots (copy -> dot -> cmult -> sub2, krylov_decomposition.f90:68-96,
+    152-186), restated in C (oracle/nekstab_oracle.c, built -Ofast like the reference's
+    bin/mks:53-55) — on the config-3 layout at ``E_sample`` elements, seeded like the GPU run
+    (hashed seed normalised with real_dot, prepare_seed).  ``seconds_per_factorisation_sample`` is
+    that measured wall time; it is scaled by N to BASELINE's N=1e8 (the steps stream the basis
+    from DRAM: linear in N; ``tools/cpu_factorisation.py`` measured the scaling on the GPU box).
+    ``fit_check``: the round-3 method (t(j) = a + b j fitted to the steps ``fit_js`` only, summed
+    over j = 1..m) evaluated on this run's own step times, with its error against the measured
+    total.  ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
 
@@ -183,30 +188,29 @@ def cpu_baseline(E_sample: int, m: int, threads: int, js, variant: str = "mgs2",
     d, _ = syn.laplacian_shift_invert(lay)
     dref = syn.to_reference_order(lay, d)
     del d
-    jmax = max(js)
-    Q = np.empty((jmax, L.len))
-    for i in range(jmax):
-        olib.orc_fill_hash(c, Q[i], 1000 + i, 0, 0)
+    Q = np.empty((m + 1, L.len))
+    Q[0] = syn.to_reference_order(lay, syn.hash_vector(lay, 11))
+    Q[0] /= np.sqrt(float(np.sum(np.concatenate([w] * lay.n_wf) * Q[0][: lay.N_w] ** 2)) + Q[0][-1] ** 2)
     f, wrk = L.zeros(), L.zeros()
-    t_step, t_mv = {}, []
-    for j in js:
-        t0 = time.perf_counter()
-        olib.orc_op_diag(c, dref, Q[j - 1], f, 0.0)
-        t1 = time.perf_counter()
-        col = np.zeros(j + 1)
-        step(c, w, col, f, Q[:j], j, wrk)
-        t_step[j] = time.perf_counter() - t1
-        t_mv.append(t1 - t0)
+    col = np.zeros(m + 1)
+    olib.orc_op_diag(c, dref, Q[0], f, 0.0)       # warm-up step (first touch of f / wrk, thread pool)
+    step(c, w, col, f, Q[:1], 1, wrk)
+    t_step = np.zeros(m)
+    t0 = time.perf_counter()
+    for j in range(1, m + 1):
+        ts = time.perf_counter()
+        olib.orc_op_diag(c, dref, Q[j - 1], f, 0.0)      # matvec(f, Q(mstep))
+        step(c, w, col, f, Q[:j], j, wrk)                # update_hessenberg_matrix
+        Q[j] = f                                         # k_copy(Q(mstep+1), f)
+        t_step[j - 1] = time.perf_counter() - ts
+    sec_fact = time.perf_counter() - t0
     olib.orc_set_threads(1)
     del Q
-    jj = np.array(sorted(t_step), dtype=np.float64)
-    tt = np.array([t_step[j] for j in sorted(t_step)])
-    if len(jj) > 1:
-        b, a = np.polyfit(jj, tt, 1)
-    else:
-        a, b = 0.0, tt[0] / jj[0]
-    mv = float(np.median(t_mv))
-    sec_fact = m * (a + mv) + b * m * (m + 1) / 2.0          # Σ_{j=1..m} [matvec + t(j)] at the sample N
+    js = [j for j in fit_js if j <= m]
+    jj = np.array(js, dtype=np.float64)
+    tt = t_step[np.array(js) - 1]
+    b, a = np.polyfit(jj, tt, 1) if len(jj) > 1 else (tt[0] / jj[0], 0.0)
+    fit_total = m * a + b * m * (m + 1) / 2.0
     scale = n_full / lay.N
     surv = survey_model_bytes(lay.N, lay.N_w, lay.n_v, m)
     refb = sum(reference_step_bytes(lay.N, lay.N_w, lay.n_v, j) for j in range(1, m + 1))
@@ -217,12 +221,14 @@ def cpu_baseline(E_sample: int, m: int, threads: int, js, variant: str = "mgs2",
         value=round(surv / sec_fact / 1e9, 2), unit="GB/s (SURVEY.md 8(d) model bytes)", cores=threads, kind="port",
         value_reference_executed_gbs=round(refb / sec_fact / 1e9, 2) if variant == "mgs2" else None,
         seconds_per_factorisation_sample=round(sec_fact, 3),
+        seconds_per_factorisation_measured=True,
         seconds_per_factorisation_N1e8=round(sec_fact * scale, 2),
-        step_seconds={int(j): round(t_step[j], 4) for j in sorted(t_step)},
-        fit_seconds={"a": float(a), "b_per_column": float(b), "matvec": mv},
-        sample=(f"{what}; config-3 layout (3-D lx1=8, {{vx,vy,vz,t}}+pr) at E={E_sample} (N={lay.N}); single "
-                f"Arnoldi steps j={list(map(int, jj))} timed on a pre-built basis, t(j)=a+b*j fitted, Σ_j over "
-                f"m={m}; seconds scaled by N to N={n_full}; {threads} thread(s) on {cpu_model()}"))
+        step_seconds={int(j): round(float(t_step[j - 1]), 4) for j in sorted(set(js + [m]))},
+        fit_check={"js": js, "fitted_total_s": round(fit_total, 3),
+                   "rel_err_vs_measured": round((fit_total - sec_fact) / sec_fact, 4)},
+        sample=(f"{what}; config-3 layout (3-D lx1=8, {{vx,vy,vz,t}}+pr) at E={E_sample} (N={lay.N}); one complete "
+                f"m={m} factorisation (matvec + update_hessenberg_matrix + k_copy per step) timed after one warm-up "
+                f"step; seconds scaled by N to N={n_full}; {threads} thread(s) on {cpu_model()}"))
 
 
 # ---- launcher ----------------------------------------------------------------------------------
@@ -306,9 +312,9 @@ def parse_args(argv=None):
                          "cgs2-native | mgs2-native (the one-call C drivers) | mgs2-icwy (MGS in inverse compact WY form)")
     ap.add_argument("--lazy-basis", action="store_true",
                     help="dcgs2 over a lazy basis Q = S T (one vector write less per step)")
-    ap.add_argument("--cpu-E", type=int, default=11044, help="CPU baseline sample (11,044 -> N=2.5e7)")
-    ap.add_argument("--cpu-js", default="1,32,64,128", help="Arnoldi steps timed on the CPU (all threads)")
-    ap.add_argument("--cpu-js-1core", default="1,8", help="... with one thread")
+    ap.add_argument("--cpu-E", type=int, default=2000,
+                    help="CPU baseline sample: one full factorisation on all threads (2,000 -> N=4.5e6, ~20 s)")
+    ap.add_argument("--cpu-E-1core", type=int, default=128, help="... with one thread (128 -> N=2.9e5)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-restart", action="store_true", help="skip the restart-rotation measurement")
     ap.add_argument("--no-ks", action="store_true", help="skip the Krylov–Schur restart leg")
@@ -415,11 +421,15 @@ def distinct_devices(devs) -> bool | None:
     return len(set(keys)) == len(keys)
 
 
-def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed):
-    """BASELINE config 3's Krylov–Schur leg at full N with restarts that really happen: the
+def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed, k_dim, schur_tgt, warmup=True):
+    """BASELINE config 3's Krylov–Schur leg at full N (k_dim=128, schur_tgt=4) on the
     shift-invert operator scaled to unit spectral radius (|mu| / max|mu|, the spectrum a
-    time-stepper exp(L dt) would present), k_dim=12, schur_tgt=4, eigen_tol=1e-10.  The oracle runs
-    the same (schur_cnt 1, mstart [9]) at reduced N (tests/test_gpu_solvers.py)."""
+    time-stepper exp(L dt) would present), the reference defaults eigen_tol=1e-6, schur_del=0.1.
+    With schur_tgt=4 the first m=128 factorisation already converges (shift-invert separates the
+    wanted end of the spectrum: no restart happens); ``schur_tgt`` above that factorisation's
+    converged count forces a real m=128 restart.  The oracle runs both at reduced N with identical
+    restart / mstart / converged-count histories
+    (tests/test_gpu_solvers.py::test_config3_krylov_schur_m128_vs_oracle)."""
     import torch
 
     from nekstab_next_amd.config import KrylovSchurConfig
@@ -427,8 +437,9 @@ def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed):
     from nekstab_next_amd.operators import DiagOperator
 
     op = DiagOperator(ctx, d_scaled)
-    cfg = KrylovSchurConfig(k_dim=12, schur_tgt=4, eigen_tol=1e-10)
-    krylov_schur(ctx, op, seed, cfg, Q=Q)       # warm-up (first-touch of small buffers)
+    cfg = KrylovSchurConfig(k_dim=k_dim, schur_tgt=schur_tgt)
+    if warmup:
+        krylov_schur(ctx, op, seed, cfg, Q=Q)       # warm-up (first-touch of small buffers)
     torch.cuda.synchronize(ctx.device)
     ctx.comm.barrier()
     t0 = time.perf_counter()
@@ -437,10 +448,12 @@ def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed):
     dt = ctx.comm.max_scalar(time.perf_counter() - t0, device=ctx.device)
     conv = res.residual < cfg.eigen_tol
     errs = [float(np.min(np.abs(exact_scaled - v)) / abs(v)) for v in res.vals[conv]]
-    return {"k_dim": 12, "schur_tgt": 4, "eigen_tol": 1e-10, "operator": "config-3 shift-invert / max|mu|",
-            "seconds": round(dt, 4), "schur_cnt": int(res.schur_cnt), "mstart_history": list(map(int, res.mstart_history)),
+    top = [float(abs(v - e) / abs(e)) for v, e in zip(res.vals[:4], exact_scaled[:4])]
+    return {"k_dim": k_dim, "schur_tgt": schur_tgt, "eigen_tol": cfg.eigen_tol,
+            "operator": "config-3 shift-invert / max|mu|", "seconds": round(dt, 4),
+            "schur_cnt": int(res.schur_cnt), "mstart_history": list(map(int, res.mstart_history)),
             "cnt_history": list(map(int, res.cnt_history)), "converged": int(res.converged),
-            "ritz_rel_err_vs_exact": max(errs) if errs else None}
+            "ritz_rel_err_vs_exact": max(errs) if errs else None, "top4_rel_err_vs_exact": max(top)}
 
 
 def run(args):
@@ -554,9 +567,12 @@ def run(args):
             "rotate_full_ms": round(full["avg_ms"], 3), "rotate_full_tflops": round(full_tf, 2),
             "rotate_full_frac_fp64": round(full_tf / FP64_PEAK_TFLOPS, 4),
         }
-    ks_leg = None
+    ks_leg = ks_restart = None
     if not args.no_ks:
-        ks_leg = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed)
+        ks_leg = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed, m, 4)
+        # schur_tgt above the first factorisation's converged count: a real m-column restart
+        ks_restart = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed, m, ks_leg["converged"] + 10,
+                                      warmup=False)
     del d_scaled
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -623,11 +639,9 @@ def run(args):
         cpu = cpu1 = cpu_opt = host = None
         if not args.no_cpu and world == 1:
             host = host_threads()
-            js = [int(x) for x in args.cpu_js.split(",")]
-            js1 = [int(x) for x in args.cpu_js_1core.split(",")]
-            cpu = cpu_baseline(args.cpu_E, m, host["threads"], js)
-            cpu1 = cpu_baseline(args.cpu_E, m, 1, js1)
-            cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], js, variant="cgs2")
+            cpu = cpu_baseline(args.cpu_E, m, host["threads"])
+            cpu1 = cpu_baseline(args.cpu_E_1core, m, 1)
+            cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], variant="cgs2")
             for c in (cpu, cpu1, cpu_opt):
                 c["gpu_ms_per_factorisation"] = round(ms_per_step, 2)
                 c["gpu_effective_gbs_same_model"] = round(effective, 2)
@@ -693,6 +707,7 @@ def run(args):
             "cpu_optimised": cpu_opt,
             "restart": restart,
             "krylov_schur_leg": ks_leg,
+            "krylov_schur_restart_leg": ks_restart,
         }
         print(json.dumps(out), file=args.json_out, flush=True)
     args.json_out.flush()

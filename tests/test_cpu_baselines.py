@@ -50,26 +50,32 @@ def test_bench_cpu_baseline_leg_small():
     import bench
 
     for variant in ("mgs2", "cgs2"):
-        r = bench.cpu_baseline(8, 6, 2, [1, 3, 6], variant=variant)
+        r = bench.cpu_baseline(8, 6, 2, variant=variant, fit_js=(1, 3, 6))
         assert {"value", "unit", "cores", "kind", "sample"} <= set(r)
         assert r["unit"].startswith("GB/s") and r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
-        assert "j=[1, 3, 6]" in r["sample"] and "m=6" in r["sample"]
-    assert "-Ofast" in bench.cpu_baseline(8, 4, 1, [1, 2])["sample"]
+        assert "one complete m=6 factorisation" in r["sample"] and "warm-up" in r["sample"]
+    assert "-Ofast" in bench.cpu_baseline(8, 4, 1)["sample"]
 
 
-def test_bench_cpu_baseline_sampled_and_extrapolated():
-    """bench.cpu_baseline times single steps on a pre-built basis, fits t(j) = a + b j and reports
-    both byte models and seconds to solution scaled to N=1e8."""
+def test_bench_cpu_baseline_measures_one_factorisation():
+    """bench.cpu_baseline times one complete m-step factorisation (measured, not
+    extrapolated from single steps), reports both byte models and seconds to solution scaled to
+    N=1e8, and the round-3 fit (steps js only) with its error against the measured total."""
     import bench
 
-    r = bench.cpu_baseline(16, 16, 2, [1, 4, 8])
+    r = bench.cpu_baseline(16, 16, 2, fit_js=(1, 4, 8, 16))
     assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+    assert r["seconds_per_factorisation_measured"] is True
     assert r["value_reference_executed_gbs"] > r["value"]        # the reference moves ~5x the model's bytes
-    assert sorted(r["step_seconds"]) == [1, 4, 8]
+    assert sorted(r["step_seconds"]) == [1, 4, 8, 16]
+    assert sum(r["step_seconds"].values()) < r["seconds_per_factorisation_sample"]
+    fc = r["fit_check"]
+    assert fc["js"] == [1, 4, 8, 16] and fc["fitted_total_s"] > 0
+    assert -1.0 < fc["rel_err_vs_measured"] < 10.0
     lay_N = box3d_layout(16).N
     assert abs(r["seconds_per_factorisation_N1e8"] / r["seconds_per_factorisation_sample"]
                - bench.N_HEADLINE / lay_N) < 0.05 * bench.N_HEADLINE / lay_N
-    o = bench.cpu_baseline(16, 16, 2, [1, 8], variant="cgs2")
+    o = bench.cpu_baseline(16, 16, 2, variant="cgs2")
     assert o["value"] > 0 and o["value_reference_executed_gbs"] is None
 
 

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_json_contract(gpu):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--E", "2000", "--steps", "2", "--warmup", "1",
-                        "--cpu-E", "64", "--cpu-js", "1,4,8", "--cpu-js-1core", "1,2"],
+                        "--cpu-E", "64", "--cpu-E-1core", "8"],
                        capture_output=True, text=True, timeout=240,
                        cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -37,8 +37,10 @@ def test_bench_json_contract(gpu):
     assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
     assert len(d["devices"]) == 1 and d["devices"][0]["pci"] and d["distinct_devices"] is True
     assert d["devices"][0]["name"]   # the marketing name, or the ISA name where libdrm has none
-    ks = d["krylov_schur_leg"]
-    assert ks["schur_cnt"] >= 1 and ks["converged"] >= 4 and ks["ritz_rel_err_vs_exact"] < 1e-10
+    ks = d["krylov_schur_leg"]   # k_dim=m=128, schur_tgt=4: converges in the first factorisation
+    assert ks["k_dim"] == 128 and ks["schur_tgt"] == 4 and ks["converged"] >= 4 and ks["top4_rel_err_vs_exact"] < 1e-10
+    kr = d["krylov_schur_restart_leg"]   # schur_tgt above that: a real 128-column restart
+    assert kr["schur_cnt"] >= 1 and kr["converged"] >= kr["schur_tgt"] and kr["top4_rel_err_vs_exact"] < 1e-10
     assert d["ritz_top8_rel_err"] < 1e-10
     assert d["gram_schmidt"]["gs_ms_per_factorisation"] <= d["ms_per_step"]
 

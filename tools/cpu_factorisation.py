@@ -1,0 +1,39 @@
+#!/usr/bin/env python
+"""One complete m=128 CPU factorisation of the reference algorithm at several sample sizes (VERDICT
+r3 item 6): bench.cpu_baseline at E = 2,000 (the bench's default sample), 4,000 and 11,044 (N=2.5e7,
+SURVEY.md §8(d)'s CPU sample) on all allowed threads, each after one warm-up step.  Shows that the
+measured seconds scale linearly in N (so the bench's E=2,000 sample, scaled to N=1e8, stands for
+the large sample) and the error of the round-3 single-step fit against each measured total.
+
+usage (GPU box host): python tools/cpu_factorisation.py OUT.json [E ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    Es = [int(x) for x in sys.argv[2:]] or [2000, 4000, 11044]
+    host = bench.host_threads()
+    rows = []
+    for E in Es:
+        r = bench.cpu_baseline(E, 128, host["threads"])
+        r["E"] = E
+        rows.append(r)
+        print(json.dumps({k: r[k] for k in ("E", "seconds_per_factorisation_sample", "seconds_per_factorisation_N1e8",
+                                            "value_reference_executed_gbs", "fit_check")}), flush=True)
+    ref = rows[-1]
+    for r in rows:
+        r["N1e8_seconds_vs_largest_sample"] = round(r["seconds_per_factorisation_N1e8"] /
+                                                    ref["seconds_per_factorisation_N1e8"] - 1.0, 4)
+    with open(out, "w") as fh:
+        json.dump({"host": host, "m": 128, "runs": rows}, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
