@@ -59,7 +59,11 @@ def _mgs2_of(mode: str) -> str:
 
 def _nonorth_of(mode: str, cfg: KrylovSchurConfig) -> str:
     """The mode for a basis that is not orthonormal (``cfg.nonorth_mode``; "mgs2" keeps a native
-    mode's library-driven variant)."""
+    mode's library-driven variant).  An explicit reference-order request (``cfg.mode`` "mgs2" /
+    "mgs2-native") is kept as it is: its rounding is the reference's, which ICWY only equals in
+    exact arithmetic."""
+    if mode in _MGS2:
+        return mode
     if cfg.nonorth_mode == "mgs2":
         return _mgs2_of(mode)
     if cfg.nonorth_mode != "mgs2-icwy":

@@ -27,6 +27,29 @@ from .operators import LegacyMatvec
 from .vector import NekContext, NekVector, k_dot, k_sub2
 
 
+def fortran_e(x: float, w: int, d: int) -> str:
+    """Fortran ``Ew.d`` edit descriptor as gfortran writes it: a 0.ddddddd mantissa, then E and a
+    signed two-digit exponent (three digits without the E above 99), right-justified in w
+    columns; e.g. E15.7 of 1.234567e-3 is ``  0.1234567E-02``."""
+    import math
+
+    if x != x:
+        return "NaN".rjust(w)
+    if math.isinf(x):
+        return ("-Infinity" if x < 0 else "Infinity").rjust(w)
+    sign = "-" if (x < 0 or (x == 0 and math.copysign(1.0, x) < 0)) else ""
+    a = abs(x)
+    if a == 0.0:
+        mant, exp = "0" * d, 0
+    else:
+        # round to d significant digits, then take the decimal exponent of the rounded value
+        m, e = f"{a:.{d - 1}e}".split("e")
+        exp = int(e) + 1
+        mant = m.replace(".", "")
+    ex = f"E{exp:+03d}" if abs(exp) <= 99 else f"{exp:+04d}"
+    return f"{sign}0.{mant}{ex}".rjust(w)
+
+
 @dataclass
 class NewtonResult:
     converged: bool
@@ -53,7 +76,7 @@ def newton_krylov(ctx: NekContext, nonlinear, linearized, q: NekVector, tol: flo
         residual = k_dot(f, f)
         res.residuals.append(residual)
         res.iterations = i
-        lines.append(f"{i:6d}{residual:15.7E}\n")
+        lines.append(f"{i:6d}{fortran_e(residual, 15, 7)}\n")   # (I6,1E15.7), newton_krylov.f90:109
         if residual < tol:
             res.converged = True
             break

@@ -58,25 +58,68 @@ def coords_from_fld(lay, files) -> dict:
     return out
 
 
+_SPLIT = 2e-4   # cells: coordinates this close across a rounding half-step are the same point
+
+
 def coincident_groups(coords: dict, rel_tol: float = 1e-9) -> tuple[np.ndarray, np.ndarray]:
     """CSR groups (start, members) of the points with equal coordinates (to ``rel_tol`` of the mesh
-    extent), groups of two or more only — the points Nek5000's gather-scatter sums over."""
+    extent), groups of two or more only — the points Nek5000's gather-scatter sums over.
+
+    Points are bucketed by their coordinates rounded to cells of ``rel_tol * extent``; two copies of
+    one GLL point that differ by a few ulps can straddle a rounding half-step and land in
+    neighbouring cells, so two points in neighbouring cells whose every coordinate agrees to
+    2e-4 cells (both then lie within 2e-4 cells of that half-step) are one group as well.  Members of a group are in ascending point order (the summation order)."""
     xs = [np.asarray(coords[k], dtype=np.float64) for k in ("x", "y", "z") if k in coords]
     n = xs[0].size
     if n == 0:
         return np.zeros(1, np.int64), np.zeros(0, np.int64)
     ext = max(float(np.ptp(x)) for x in xs) or 1.0
-    keys = [np.round(x / (rel_tol * ext)).astype(np.int64) for x in xs]
+    tol = rel_tol * ext
+    sc = [x / tol for x in xs]
+    keys = [np.round(v).astype(np.int64) for v in sc]
     order = np.lexsort(keys[::-1])
     ks = np.stack([k[order] for k in keys], axis=1)
     new = np.ones(n, dtype=bool)
     new[1:] = np.any(ks[1:] != ks[:-1], axis=1)
-    gid = np.cumsum(new) - 1
+    gid = np.empty(n, dtype=np.int64)
+    gid[order] = np.cumsum(new) - 1
+    near = [np.abs(v - np.floor(v) - 0.5) <= _SPLIT for v in sc]
+    flagged = np.flatnonzero(np.any(near, axis=0))
+    if flagged.size:
+        # a split pair lies within 1e-4 cells of the same half-step on either side: both flagged
+        table = {}
+        for p in flagged.tolist():
+            table.setdefault(tuple(int(k[p]) for k in keys), []).append(p)
+        parent = {}
+
+        def find(g):
+            while parent.get(g, g) != g:
+                g = parent[g]
+            return g
+
+        for p in flagged.tolist():
+            kp = [int(k[p]) for k in keys]
+            cs = [c for c in range(len(xs)) if near[c][p]]
+            for mask in range(1, 1 << len(cs)):
+                alt = list(kp)
+                for b, c in enumerate(cs):
+                    if mask >> b & 1:
+                        alt[c] += 1 if sc[c][p] > kp[c] else -1
+                for q in table.get(tuple(alt), ()):
+                    if all(abs(x[p] - x[q]) <= _SPLIT * tol for x in xs):
+                        a, b2 = find(int(gid[p])), find(int(gid[q]))
+                        if a != b2:
+                            parent[max(a, b2)] = min(a, b2)
+        if parent:
+            roots = {g: find(g) for g in list(parent)}
+            moved = np.array(list(roots), dtype=np.int64)
+            lut = np.arange(int(gid.max()) + 1, dtype=np.int64)
+            lut[moved] = np.array([roots[g] for g in moved.tolist()], dtype=np.int64)
+            gid = lut[gid]
     counts = np.bincount(gid)
-    multi = counts[gid] > 1
-    # lexsort is stable: inside a group the points stay in ascending order (the summation order)
-    members = order[multi].astype(np.int64)
-    g_multi = gid[multi]
+    idx = np.flatnonzero(counts[gid] > 1)                 # ascending point order
+    members = idx[np.lexsort((idx, gid[idx]))].astype(np.int64)
+    g_multi = gid[members]
     starts = np.flatnonzero(np.r_[True, g_multi[1:] != g_multi[:-1]]) if members.size else np.zeros(0, np.int64)
     return np.r_[starts, members.size].astype(np.int64), members
 
@@ -180,13 +223,16 @@ def noise_seed(ctx: NekContext, coords: dict, ifto: bool | None = None, ifpsco=(
     return seed
 
 
-def symmetric_seed(ctx: NekContext, coords: dict, base: NekVector | None = None) -> NekVector:
+def symmetric_seed(ctx: NekContext, coords: dict, base: NekVector | None = None, bm1=None) -> NekVector:
     """``add_symmetric_seed(wrk%vx, wrk%vy, wrk%vz, wrk%t(:,1))`` (utils.f90:361-406, called at
     eigensolvers.f90:205-208 when ``ifseed_symm``): on a copy of ``base`` (zero by default) vx, vz
     and t(:,1) become cos(alpha z) sin(2 pi y), -(2 pi / alpha) cos(alpha z) cos(2 pi y) and
     cos(alpha z) cos(2 pi y) with alpha = 2 pi / (zmax - zmin) over all ranks; vy keeps the base's
     values (the reference never writes qy); then vx, vy, vz and t(:,1) are scaled by
-    1e-6 / (0.5 sum_c glsc3(q_c, bm1, q_c)) over the velocity components (bm1: the context's weights).
+    1e-6 / (0.5 sum_c glsc3(q_c, bm1, q_c)) over the velocity components.  ``bm1``: the mass matrix
+    (this rank's n_v points) when the context's dot weights are not bm1 — with a sponge the
+    context holds bm1s, zero in the sponge (forcing.f90:101-104), while add_symmetric_seed
+    weights with bm1 (utils.f90:394-396); default: the context's weights.
     The in-tree solver takes the result as Q(1) unnormalised (``seed_mode="symm"``).  3-D with a
     scalar field only (in 2-D the reference divides by zmax - zmin = 0)."""
     lay = ctx.layout
@@ -208,7 +254,17 @@ def symmetric_seed(ctx: NekContext, coords: dict, base: NekVector | None = None)
     vel = ctx.vector()
     vel.copy_from(seed)
     vel.storage[3 * sv:lay.n_wf * sv].zero_()       # amp over vx, vy, vz only (glsc3 x 3, :394-396)
-    amp = ctx.dot(vel, vel, time=False)
+    if bm1 is None:
+        amp = ctx.dot(vel, vel, time=False)
+    else:
+        b = np.asarray(bm1, dtype=np.float64).ravel()
+        if b.size < lay.n_v:
+            raise ValueError(f"bm1 holds {b.size} points, the shard has n_v={lay.n_v}")
+        wb = torch.zeros(max(lay.sv, 4096), dtype=torch.float64, device=ctx.device)
+        wb[: lay.n_v] = torch.as_tensor(b[: lay.n_v])
+        out = ctx.scal[1:2]
+        ctx.call("nkv_dot", wb.data_ptr(), vel.ptr, vel.ptr, out.data_ptr(), ctx.ws.data_ptr(), 0, ctx.stream)
+        amp = float(ctx.comm.allreduce_(out).item())
     amp = 1e-6 / (0.50 * amp)
     for c in (0, 1, 2, 3):                          # opcmult(qx, qy, qz, amp); cmult(qp, amp)
         seg = seed.storage[c * sv:(c + 1) * sv]

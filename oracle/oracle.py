@@ -840,15 +840,41 @@ def glsc3_np(a, w, b):
 def coincident_average(q, coords, rel_tol=1e-9):
     """dssum followed by vmult on one rank (Nek5000 gs '+', then the inverse multiplicity): every
     point gets the mean of the points with the same coordinates, summed in ascending point order
-    and scaled by 1/count.  Independent grouping (a dict on rounded coordinates)."""
+    and scaled by 1/count.  Independent grouping: a dict on rounded coordinates, then every cell is
+    joined with each of its 3^d - 1 neighbour cells holding a point that agrees with one of its own
+    to 2e-4 cells in every coordinate (two copies of a point a few ulps apart can round to
+    neighbouring cells)."""
+    import itertools
+
     xs = [np.asarray(coords[k]) for k in ("x", "y", "z") if k in coords]
     ext = max(float(np.ptp(a)) for a in xs) or 1.0
-    groups = {}
+    tol = rel_tol * ext
+    cells = {}
     for p in range(xs[0].size):
-        key = tuple(int(round(float(a[p]) / (rel_tol * ext))) for a in xs)
-        groups.setdefault(key, []).append(p)
+        key = tuple(int(round(float(a[p]) / tol)) for a in xs)
+        cells.setdefault(key, []).append(p)
+    root = {k: k for k in cells}
+
+    def find(k):
+        while root[k] != k:
+            k = root[k]
+        return k
+
+    for key, pts in cells.items():
+        for off in itertools.product((-1, 0, 1), repeat=len(xs)):
+            nb = tuple(a + b for a, b in zip(key, off))
+            if nb == key or nb not in cells:
+                continue
+            if any(all(abs(float(a[p]) - float(a[r])) <= 2e-4 * tol for a in xs) for p in pts for r in cells[nb]):
+                ra, rb = find(key), find(nb)
+                if ra != rb:
+                    root[max(ra, rb)] = min(ra, rb)
+    groups = {}
+    for key, pts in cells.items():
+        groups.setdefault(find(key), []).extend(pts)
     out = q.copy()
     for members in groups.values():
+        members = sorted(members)
         if len(members) < 2:
             continue
         s = 0.0

@@ -204,3 +204,25 @@ def test_symmetric_seed_vs_oracle(gpu):
         assert np.min(np.abs(res.vals - v)) <= 1e-10 * abs(v)
     with pytest.raises(ValueError):
         seeds.symmetric_seed(NekContext(cylinder_layout(20), max_cols=4), {"x": np.zeros(720), "y": np.zeros(720)})
+
+
+def test_symmetric_seed_amplitude_with_sponge_uses_bm1(gpu):
+    """With a sponge the context's dot weights are bm1s (zero in the sponge, forcing.f90:101-104),
+    but add_symmetric_seed's amplitude weights with bm1 (utils.f90:394-396): passing ``bm1`` gives
+    the oracle's seed computed with bm1; without it the amplitude follows the context's bm1s."""
+    from nekstab_next_amd import synthetic as syn
+
+    lay, co = _cases()["box3d"]
+    w = syn.mass_weights(lay)
+    ws = syn.sponge(w)
+    assert np.any(ws[: lay.n_v] == 0.0) and np.any(ws[: lay.n_v] != 0.0)
+    ctx = NekContext(lay, weights=ws, max_cols=4)
+    base = ctx.vector()
+    base.fill_hash(9)
+    qy = base.to_packed()[lay.sv: lay.sv + lay.n_v]
+    for bm1, wref in ((w, w), (None, ws)):
+        got = seeds.symmetric_seed(ctx, co, base, bm1=bm1).to_packed()
+        ref = orc.add_symmetric_seed(co["y"], co["z"], qy, wref[: lay.n_v], co["z"].min(), co["z"].max())
+        for c, r in zip((0, 1, 2, 3), ref):
+            g = got[c * lay.sv: c * lay.sv + lay.n_v]
+            np.testing.assert_allclose(g, r, rtol=0, atol=1e-13 * np.max(np.abs(r)))

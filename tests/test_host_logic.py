@@ -195,3 +195,29 @@ def test_givens_column_rejects_bad_input():
     assert np.isnan(lib.nkv_givens_column(0, None, p, p, p))
     assert "givens" in _lib.last_error()
     assert not np.isnan(lib.nkv_givens_column(0, p, p, p, p))
+
+
+def test_residu_newton_fortran_e_format():
+    """residu_newton.dat is written (I6,1E15.7) (newton_krylov.f90:109): gfortran's Ew.d form,
+    0.ddddddd mantissa and a signed two-digit exponent."""
+    from nekstab_next_amd.newton import fortran_e
+
+    assert f"{3:6d}{fortran_e(1.234567e-3, 15, 7)}" == "     3  0.1234567E-02"
+    assert fortran_e(0.0, 15, 7) == "  0.0000000E+00"
+    assert fortran_e(-2.5, 15, 7) == " -0.2500000E+01"
+    assert fortran_e(0.999999999, 15, 7) == "  0.1000000E+01"     # rounding carries into the exponent
+    assert fortran_e(4.56e-120, 15, 7) == "  0.4560000-119"       # three-digit exponent drops the E
+    assert fortran_e(123.456789, 15, 7) == "  0.1234568E+03"
+
+
+def test_explicit_reference_order_kept_for_nonorthonormal_bases():
+    """A noise/load/symm seed runs modified Gram–Schmidt; an explicit request for the reference's
+    own order (mode "mgs2" / "mgs2-native") is kept, not replaced by the ICWY form."""
+    from nekstab_next_amd.config import KrylovSchurConfig
+    from nekstab_next_amd.krylov_schur import _MGS2, _nonorth_of
+
+    cfg = KrylovSchurConfig()
+    assert cfg.nonorth_mode == "mgs2-icwy"
+    assert _nonorth_of("mgs2", cfg) == "mgs2" and _nonorth_of("mgs2-native", cfg) == "mgs2-native"
+    assert _nonorth_of("dcgs2", cfg) == "mgs2-icwy" and _nonorth_of("dcgs2-native", cfg) == "mgs2-icwy-native"
+    assert _nonorth_of("cgs2", KrylovSchurConfig(nonorth_mode="mgs2")) in _MGS2

@@ -82,6 +82,29 @@ def test_coincident_groups_vs_oracle(case):
     assert sizes.min() >= 2 and sizes.max() == (5 if case == "cyl" else 8)
 
 
+def test_coincident_groups_across_a_rounding_half_step():
+    """Two copies of one point a few ulps apart on either side of a rounding half-step of the
+    grouping grid (cells of 1e-9 x extent) are one group: in x, in y, and in both; the
+    oracle's independent grouping agrees, and points 0.01 cells apart stay apart."""
+    ext = 1.0
+    tol = 1e-9 * ext
+    c = (123456 + 0.5) * tol
+    lo, hi = np.nextafter(c, -1.0), np.nextafter(np.nextafter(c, 2.0), 2.0)
+    assert int(np.round(lo / tol)) != int(np.round(hi / tol))   # the pair does straddle the half-step
+    far = c + 0.01 * tol
+    x = np.array([0.0, ext, lo, hi, 0.3, 0.3, lo, hi, 0.7, far, c - 0.2 * tol])
+    y = np.array([0.0, ext, 0.5, 0.5, lo, hi, lo, hi, 0.1, 0.9, 0.9])
+    co = {"x": x, "y": y}
+    start, members = seeds.coincident_groups(co)
+    groups = sorted([int(i) for i in members[a:b]] for a, b in zip(start[:-1], start[1:]))
+    assert groups == [[2, 3], [4, 5], [6, 7]], groups
+    q = np.random.default_rng(3).standard_normal(x.size)
+    got = q.copy()
+    for g in groups:
+        got[g] = (q[g[0]] + q[g[1]]) * 0.5
+    np.testing.assert_array_equal(got, orc.coincident_average(q, co))
+
+
 def test_coords_from_fld_element_map(tmp_path):
     """Mesh coordinates from a field file whose element map is permuted (as BF_1cyl0.f00001's is:
     50, 51, ...), on one rank and as the shard of rank 1 of 3."""
