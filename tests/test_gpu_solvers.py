@@ -111,7 +111,8 @@ def test_config3_krylov_schur_m128_vs_oracle(gpu, mode, tgt, schur_cnt):
     on this operator family: shift-invert separates the wanted end of the spectrum); schur_tgt=90
     (more than one factorisation converges) forces a real m=128 restart: 80 columns kept (the MFMA
     slab rotation), 47 new steps.  Restart count, mstart and converged-count histories identical
-    to the oracle's MGS2 run; comparison-set Ritz values 1e-10; top 4 vs the exact spectrum."""
+    to the oracle's MGS2 run; Ritz values 1e-10 where relatively converged (see below); top 4 vs
+    the exact spectrum."""
     lay = box3d_layout(128)
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=136)
@@ -124,7 +125,21 @@ def test_config3_krylov_schur_m128_vs_oracle(gpu, mode, tgt, schur_cnt):
     ref = _oracle_once(("c3m128", tgt), lambda: orc.krylov_schur(
         L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d / rho)), q1, 128, tgt))
     assert ref["schur_cnt"] == schur_cnt
-    _compare_ks(res, ref, cfg)
+    assert res.schur_cnt == ref["schur_cnt"] and res.mstart_history == ref["mstart"]
+    assert res.cnt_history == ref["cnt"]
+    # eigen_tol is absolute (eigensolvers.f90:309-310): on this spectrum it also admits Ritz values
+    # near zero (|mu| down to ~1e-9 of the spectral radius, residuals up to ~30x their size); those
+    # are gated in absolute terms (1e-10 of |mu_1|), the relatively converged ones (residual
+    # < 1e-6 |mu|: 72 and 87 of the 80 and 93) and the top 8 at 1e-10 relative
+    rv, rr = ref["vals"], ref["residual"]
+    tight = np.array(sorted(set(np.nonzero(rr < 1e-6 * np.abs(rv))[0].tolist()) | set(range(8))))
+    loose = np.array(sorted(set(np.nonzero(rr < cfg.eigen_tol)[0].tolist()) - set(tight.tolist())), dtype=int)
+    got = match_ritz(rv[tight], res.vals)
+    assert np.max(np.abs(got - rv[tight]) / np.abs(rv[tight])) <= 1e-10
+    assert tight.size >= 60
+    if loose.size:
+        got = match_ritz(rv[loose], res.vals)
+        assert np.max(np.abs(got - rv[loose])) <= 1e-10 * np.abs(rv[0])
     np.testing.assert_allclose(res.vals[:4].real, exact[:4] / rho, rtol=1e-10)
 
 
