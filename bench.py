@@ -446,13 +446,17 @@ def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed, k_dim, schur_tgt
     res = krylov_schur(ctx, op, seed, cfg, Q=Q)
     torch.cuda.synchronize(ctx.device)
     dt = ctx.comm.max_scalar(time.perf_counter() - t0, device=ctx.device)
-    conv = res.residual < cfg.eigen_tol
-    errs = [float(np.min(np.abs(exact_scaled - v)) / abs(v)) for v in res.vals[conv]]
+    # eigen_tol is absolute (eigensolvers.f90:309-310): besides the wanted end it counts Ritz values
+    # near zero whose residual is small only because they are; the accuracy is reported over the
+    # relatively converged ones (residual < 1e-6 |mu|), all of them among the exact 4096 largest
+    rel = res.residual < 1e-6 * np.abs(res.vals)
+    errs = [float(np.min(np.abs(exact_scaled - v)) / abs(v)) for v in res.vals[rel]]
     top = [float(abs(v - e) / abs(e)) for v, e in zip(res.vals[:4], exact_scaled[:4])]
     return {"k_dim": k_dim, "schur_tgt": schur_tgt, "eigen_tol": cfg.eigen_tol,
             "operator": "config-3 shift-invert / max|mu|", "seconds": round(dt, 4),
             "schur_cnt": int(res.schur_cnt), "mstart_history": list(map(int, res.mstart_history)),
             "cnt_history": list(map(int, res.cnt_history)), "converged": int(res.converged),
+            "relatively_converged": int(rel.sum()),
             "ritz_rel_err_vs_exact": max(errs) if errs else None, "top4_rel_err_vs_exact": max(top)}
 
 
