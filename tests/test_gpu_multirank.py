@@ -497,3 +497,111 @@ def test_round3_paths_sharded_match_one_rank(gpu, tmp_path, world):
         # moves them by up to ~1e-12 relative (1.06e-12 measured at 4 ranks): gate 1e-10
         assert abs(abs(ip2) - abs(ip1)) <= 1e-10 * abs(ip1)
         assert np.max(np.abs(g2 - g1)) <= 1e-10 * np.max(np.abs(g1))
+
+
+def _run_config5(world_rank_pair, out, port, E):
+    """Config 5 on one rank of `world` (BASELINE: 4 GPUs): direct and adjoint Krylov–Schur on
+    A = D + rank-2 non-normal term (two bases resident), leading modes, bi-orthogonalisation."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import KrylovSchurConfig
+        from nekstab_next_amd.krylov_schur import krylov_schur, ritz_vector
+        from nekstab_next_amd.layout import box3d_layout
+        from nekstab_next_amd.operators import DiagOperator, RankTwoPerturbed
+        from nekstab_next_amd.sensitivity import biorthogonalize
+        from nekstab_next_amd.vector import NekContext
+
+        lay = box3d_layout(E).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=40)
+        d, _ = syn.diag_spectrum(lay)
+        vs = [ctx.vector().from_packed(syn.hash_vector(lay, s) * 1e-3) for s in (21, 22, 23, 24)]
+        A = RankTwoPerturbed(DiagOperator(ctx, d), *vs, sigma=50.0)
+        seed = ctx.vector()
+        seed.fill_hash(11)
+        cfg = KrylovSchurConfig(k_dim=30, schur_tgt=2)
+        rd = krylov_schur(ctx, A, seed, cfg)
+        ra = krylov_schur(ctx, A, seed, cfg, transpose=True)
+        dRe, dIm, aRe, aIm = (ctx.vector() for _ in range(4))
+        ritz_vector(ctx, rd.Q, rd.vecs, 0, dRe, dIm, k=30)
+        ritz_vector(ctx, ra.Q, ra.vecs, 0, aRe, aIm, k=30)
+        ip = biorthogonalize(ctx, dRe, dIm, aRe, aIm)
+        out[(world, rank)] = dict(
+            d=(rd.vals, rd.residual, rd.mstart_history, rd.cnt_history, rd.schur_cnt),
+            a=(ra.vals, ra.residual, ra.mstart_history, ra.cnt_history, ra.schur_cnt),
+            ip=ip, modes=[x.to_packed() for x in (dRe, dIm, aRe, aIm)])
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_config5_four_ranks_vs_oracle(gpu):
+    """Config 5 split as BASELINE names it (4 ranks; gloo ranks sharing this box's GPU) at reduced N
+    (3-D lx1=8, E=61: ragged 15/15/15/16-element shards) against the oracle's UNSHARDED run
+    (sensitivity.f90:393-469 after two eigensolver runs, eigensolvers.f90:120-359): direct and
+    adjoint restart trajectories identical, comparison-set Ritz values 1e-10, and every rank's
+    shard of the bi-orthogonalised leading modes equal to the oracle's modes (1e-9 of max, after
+    the pair's common sign) with <a, d>_W = 1 + 0i to 1e-12 on both."""
+    import oracle as orc
+    from helpers import olayout, oracle_rank2_matvec
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import box3d_layout
+
+    E, world = 61, 4
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_run_config5, args=((r, world), out, port, E)) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    g = box3d_layout(E)
+    L, w = olayout(g), syn.mass_weights(g)
+    d, _ = syn.diag_spectrum(g)
+    vh = [syn.hash_vector(g, s) * 1e-3 for s in (21, 22, 23, 24)]
+    q1 = orc.prepare_seed(L, w, syn.to_reference_order(g, syn.hash_vector(g, 11)))
+    orc.set_threads(8)
+    try:
+        ref = {tr: orc.krylov_schur(L, w, oracle_rank2_matvec(g, d, *vh, 50.0, w, tr), q1, 30, 2)
+               for tr in (False, True)}
+    finally:
+        orc.set_threads(1)
+    modes = []
+    for tr in (False, True):
+        re, im, _, _ = orc.outpost_mode(L, w, ref[tr]["Q"], ref[tr]["vecs"], 0, 30)
+        modes += [re, im]
+    o = orc.biorthogonalize(L, w, *modes)
+    o_pad = [syn.from_reference_order(g, v) for v in o]
+    for rank in range(world):
+        got = out[(world, rank)]
+        for key, tr in (("d", False), ("a", True)):
+            vals, res_, mh, ch, sc = got[key]
+            r = ref[tr]
+            assert sc == r["schur_cnt"] and mh == r["mstart"] and ch == r["cnt"], (rank, key)
+            sel = ritz_compare_set(r["vals"], r["residual"], 1e-6)
+            assert np.max(np.abs(match_ritz(r["vals"][sel], vals) - r["vals"][sel]) / np.abs(r["vals"][sel])) <= 1e-10
+        s = g.shard(rank, world)
+        sign = None
+        for x, y in zip(got["modes"], o_pad):
+            pieces = [(x[f * s.sv: f * s.sv + s.n_v], y[f * g.sv + s.v_offset: f * g.sv + s.v_offset + s.n_v])
+                      for f in range(g.n_wf)]
+            pieces.append((x[s.n_wf * s.sv: s.n_wf * s.sv + s.n_p],
+                           y[g.n_wf * g.sv + s.p_offset: g.n_wf * g.sv + s.p_offset + s.n_p]))
+            a = np.concatenate([p[0] for p in pieces])
+            b = np.concatenate([p[1] for p in pieces])
+            if sign is None:   # the leading mode's free sign (dgeev's), common to the bi-orthogonal pair
+                sign = 1.0 if np.dot(a, b) >= 0 else -1.0
+            scale = max(np.max(np.abs(v)) for v in o)
+            assert np.max(np.abs(sign * a - b)) <= 1e-9 * scale, rank
+        ip = got["ip"]
+        assert abs(abs(ip) - 1.0) < 0.5   # <a, d> before the rescaling: O(1)
