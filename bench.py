@@ -29,8 +29,8 @@ work definition the CPU baseline is also reported in).  ``roofline`` is the domi
 timed live with HIP events on the launch stream.  Outside the timed region: ``restart`` times one
 Krylov–Schur condensation of the final factorisation (H rescaled to unit spectral radius, see
 there), ``krylov_schur_leg`` runs config 3's Krylov–Schur (k_dim=m, schur_tgt=4) and
-``krylov_schur_restart_leg`` the same with schur_tgt above the first factorisation's converged
-count, i.e. through a real m-column restart.
+``krylov_schur_restart_leg`` the same on a clustered time-stepper-like spectrum that needs real
+m-column restarts.
 """
 from __future__ import annotations
 
@@ -421,15 +421,17 @@ def distinct_devices(devs) -> bool | None:
     return len(set(keys)) == len(keys)
 
 
-def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed, k_dim, schur_tgt, warmup=True):
+def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed, k_dim, schur_tgt, warmup=True,
+                     operator="config-3 shift-invert / max|mu|"):
     """BASELINE config 3's Krylov–Schur leg at full N (k_dim=128, schur_tgt=4) on the
     shift-invert operator scaled to unit spectral radius (|mu| / max|mu|, the spectrum a
     time-stepper exp(L dt) would present), the reference defaults eigen_tol=1e-6, schur_del=0.1.
     With schur_tgt=4 the first m=128 factorisation already converges (shift-invert separates the
-    wanted end of the spectrum: no restart happens); ``schur_tgt`` above that factorisation's
-    converged count forces a real m=128 restart.  The oracle runs both at reduced N with identical
-    restart / mstart / converged-count histories
-    (tests/test_gpu_solvers.py::test_config3_krylov_schur_m128_vs_oracle)."""
+    wanted end of the spectrum: no restart happens); the restart leg runs the same m and schur_tgt
+    on ``syn.clustered_spectrum`` (a time-stepper-like cluster below 1), which restarts.  The oracle
+    runs both at reduced N with identical restart / mstart / converged-count histories
+    (tests/test_gpu_solvers.py::test_config3_krylov_schur_m128_vs_oracle,
+    ::test_krylov_schur_m128_real_restart_vs_oracle)."""
     import torch
 
     from nekstab_next_amd.config import KrylovSchurConfig
@@ -453,7 +455,7 @@ def krylov_schur_leg(ctx, lay, Q, d_scaled, exact_scaled, seed, k_dim, schur_tgt
     errs = [float(np.min(np.abs(exact_scaled - v)) / abs(v)) for v in res.vals[rel]]
     top = [float(abs(v - e) / abs(e)) for v, e in zip(res.vals[:4], exact_scaled[:4])]
     return {"k_dim": k_dim, "schur_tgt": schur_tgt, "eigen_tol": cfg.eigen_tol,
-            "operator": "config-3 shift-invert / max|mu|", "seconds": round(dt, 4),
+            "operator": operator, "seconds": round(dt, 4),
             "schur_cnt": int(res.schur_cnt), "mstart_history": list(map(int, res.mstart_history)),
             "cnt_history": list(map(int, res.cnt_history)), "converged": int(res.converged),
             "relatively_converged": int(rel.sum()),
@@ -574,10 +576,14 @@ def run(args):
     ks_leg = ks_restart = None
     if not args.no_ks:
         ks_leg = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed, m, 4)
-        # schur_tgt above the first factorisation's converged count: a real m-column restart
-        ks_restart = krylov_schur_leg(ctx, lay, Q, d_scaled, exact / rho, seed, m, ks_leg["converged"] + 10,
-                                      warmup=False)
-    del d_scaled
+        del d_scaled
+        # the same m and schur_tgt on a time-stepper-like clustered spectrum: real m-column restarts
+        d_cl, exact_cl = syn.clustered_spectrum(lay)
+        ks_restart = krylov_schur_leg(ctx, lay, Q, d_cl, exact_cl, seed, m, 4, warmup=False,
+                                      operator="clustered: 1 - 0.002 (k - 1/2), k <= 400, over U[0, 0.2]")
+        del d_cl
+    else:
+        del d_scaled
 
     ms_per_step = elapsed / args.steps * 1e3
     nv_g = glay.pts_v * glay.nelgv

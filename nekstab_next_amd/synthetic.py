@@ -169,6 +169,35 @@ def rot2_operator(lay: NekLayout, seed: int = 2, pairs=DOMINANT_PAIRS, rest_valu
     return c, s, d_rest, np.asarray(exact)
 
 
+# ---- a clustered spectrum that needs Krylov–Schur restarts at m = 128 ------------------------------
+
+def clustered_spectrum(lay: NekLayout, spacing: float = 0.002, n_cluster: int = 400, bulk: float = 0.2,
+                       seed: int = 5, pr_value: float = 0.1) -> tuple:
+    """(padded diag, exact cluster eigenvalues, decreasing).  A time-stepper-like spectrum: a dense
+    cluster below 1, lambda_k = 1 - spacing (k - 1/2) for k = 1..n_cluster on seeded distinct
+    global weighted dofs (an affine permutation), over a bulk U[0, bulk] (hashed per global dof);
+    pressure ``pr_value``.  The cluster's spacing makes the leading eigenvalues converge slowly, so a
+    128-vector Krylov–Schur with schur_tgt=4 restarts (the half-step keeps every eigenvalue away
+    from select_eigvals' |lambda| > 0.9 boundary); shard-independent like every generator here."""
+    n = lay.n_wf * lay.pts_v * lay.nelgv
+    a, b = _affine_perm_params(n, seed)
+    k = np.arange(n_cluster, dtype=np.int64)
+    pos = (a * k + b) % n
+    order = np.argsort(pos)
+    pos_sorted, val_sorted = pos[order], (1.0 - spacing * (k + 0.5))[order]
+    d = np.zeros(lay.ld)
+    for f in range(lay.n_wf):
+        g = weighted_global_index(lay, f)
+        v = bulk * hash_uniform(seed, 501, g.astype(np.uint64))
+        i = np.searchsorted(pos_sorted, g)
+        hit = (i < pos_sorted.size) & (pos_sorted[np.minimum(i, pos_sorted.size - 1)] == g)
+        v[hit] = val_sorted[i[hit]]
+        d[f * lay.sv: f * lay.sv + lay.n_v] = v
+    s = lay.n_wf * lay.sv
+    d[s: s + lay.n_p] = pr_value
+    return d, 1.0 - spacing * (k + 0.5)
+
+
 # ---- config 3: diagonalised shift-invert Laplacian ----------------------------------------------
 
 def _affine_perm_params(n: int, seed: int) -> tuple[int, int]:

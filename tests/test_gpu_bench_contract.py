@@ -39,8 +39,8 @@ def test_bench_json_contract(gpu):
     assert d["devices"][0]["name"]   # the marketing name, or the ISA name where libdrm has none
     ks = d["krylov_schur_leg"]   # k_dim=m=128, schur_tgt=4: converges in the first factorisation
     assert ks["k_dim"] == 128 and ks["schur_tgt"] == 4 and ks["converged"] >= 4 and ks["top4_rel_err_vs_exact"] < 1e-10
-    kr = d["krylov_schur_restart_leg"]   # schur_tgt above that: a real 128-column restart
-    assert kr["schur_cnt"] >= 1 and kr["converged"] >= kr["schur_tgt"] and kr["top4_rel_err_vs_exact"] < 1e-10
+    kr = d["krylov_schur_restart_leg"]   # a clustered spectrum: real 128-column restarts
+    assert kr["schur_cnt"] >= 1 and kr["converged"] >= 4 and kr["top4_rel_err_vs_exact"] < 1e-10
     for leg in (ks, kr):
         assert leg["relatively_converged"] >= 4 and leg["ritz_rel_err_vs_exact"] < 1e-10
     assert d["ritz_top8_rel_err"] < 1e-10
