@@ -39,19 +39,21 @@ def _init(rank, world, port):
 
 
 def _race_worker(rank, world, port, directory, barrier, late, reader_comm, out):
+    sys.path.insert(0, ROOT)
+    from nekstab_next_amd import fld   # imports and data before the rendezvous: the ranks leave it together
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.comm import Comm
+    from nekstab_next_amd.layout import box3d_layout
+
+    lay = box3d_layout(23).shard(rank, world)
+    f = fld.fld_from_vector(lay, syn.hash_vector(lay, 4), time=1.0, istep=1)
     _init(rank, world, port)
     try:
-        from nekstab_next_amd import fld
-        from nekstab_next_amd import synthetic as syn
-        from nekstab_next_amd.comm import Comm
-        from nekstab_next_amd.layout import box3d_layout
-
         comm = Comm()
-        lay = box3d_layout(23).shard(rank, world)
+        comm.barrier()
         with fld.collective_output(comm, barrier=barrier):
             if rank == late:
-                time.sleep(1.5)   # the slowest writer (rank 0 also writes the Spectre_* text)
-            f = fld.fld_from_vector(lay, syn.hash_vector(lay, 4), time=1.0, istep=1)
+                time.sleep(3.0)   # the slowest writer (rank 0 also writes the Spectre_* text)
             fld.write_fld(os.path.join(directory, fld.fld_name("aRe", "mr", rank, 1)), f)
         try:
             # as wave_maker's _load_modes: this rank's elements of the set (reader_comm: the
@@ -69,7 +71,7 @@ def _race_worker(rank, world, port, directory, barrier, late, reader_comm, out):
 @pytest.mark.parametrize("barrier,late,reader_comm", [(True, 0, True), (True, 3, False), (False, 0, False),
                                                       (False, 3, False)])
 def test_delayed_writer_needs_the_barrier(tmp_path, barrier, late, reader_comm):
-    """Rank `late` writes its member 1.5 s after the others.  Late rank 0 is the round-3 failure
+    """Rank `late` writes its member 3 s after the others.  Late rank 0 is the round-3 failure
     (the readers race rank 0's file); late rank 3 is the same race on a member other than the
     header's.  Without the barrier the independent readers fail (the product's collective read
     broadcasts the set header from rank 0; whether that broadcast also waits for the late rank is
