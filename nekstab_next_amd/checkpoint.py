@@ -71,7 +71,8 @@ def read_hes(path: str, mstart: int, k_dim: int) -> np.ndarray:
     if mstart < 1:
         raise ValueError(f"mstart={mstart} < 1")
     need = (mstart + 1) * mstart
-    A = _list_directed_reals(open(path).read(), need, path).reshape(mstart + 1, mstart)
+    with open(path) as fh:
+        A = _list_directed_reals(fh.read(), need, path).reshape(mstart + 1, mstart)
     H = np.zeros((k_dim + 1, k_dim), order="F")
     H[: mstart + 1, :mstart] = A
     return H
