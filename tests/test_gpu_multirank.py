@@ -533,10 +533,16 @@ def _run_config5(world_rank_pair, out, port, E):
         ritz_vector(ctx, rd.Q, rd.vecs, 0, dRe, dIm, k=30)
         ritz_vector(ctx, ra.Q, ra.vecs, 0, aRe, aIm, k=30)
         ip = biorthogonalize(ctx, dRe, dIm, aRe, aIm)
+        # norm_grad on the shard (gradm1 element-local, one all-reduced dot): the filter's number
+        from seed_helpers import box_mesh_coords
+
+        from nekstab_next_amd.sensitivity import NormGrad
+
+        ng = NormGrad(ctx, box_mesh_coords(lay, (E, 1, 1)))(dRe)
         out[(world, rank)] = dict(
             d=(rd.vals, rd.residual, rd.mstart_history, rd.cnt_history, rd.schur_cnt),
             a=(ra.vals, ra.residual, ra.mstart_history, ra.cnt_history, ra.schur_cnt),
-            ip=ip, modes=[x.to_packed() for x in (dRe, dIm, aRe, aIm)])
+            ip=ip, modes=[x.to_packed() for x in (dRe, dIm, aRe, aIm)], norm_grad=ng)
     finally:
         if world > 1:
             dist.destroy_process_group()
@@ -548,7 +554,8 @@ def test_config5_four_ranks_vs_oracle(gpu):
     (sensitivity.f90:393-469 after two eigensolver runs, eigensolvers.f90:120-359): direct and
     adjoint restart trajectories identical, comparison-set Ritz values 1e-10, and every rank's
     shard of the bi-orthogonalised leading modes equal to the oracle's modes (1e-9 of max, after
-    the pair's common sign) with <a, d>_W = 1 + 0i to 1e-12 on both."""
+    the pair's common sign) with <a, d>_W = 1 + 0i to 1e-12 on both; the spurious-mode filter's
+    norm_grad of the direct mode, computed on the shards, equals the oracle's on the whole mesh."""
     import oracle as orc
     from helpers import olayout, oracle_rank2_matvec
     from nekstab_next_amd import synthetic as syn
@@ -582,6 +589,9 @@ def test_config5_four_ranks_vs_oracle(gpu):
         modes += [re, im]
     o = orc.biorthogonalize(L, w, *modes)
     o_pad = [syn.from_reference_order(g, v) for v in o]
+    from seed_helpers import box_mesh_coords
+
+    ng_ref = orc.norm_grad(g.lx1, 3, box_mesh_coords(g, (E, 1, 1)), w, [o[0][c * g.n_v:(c + 1) * g.n_v] for c in range(3)])
     for rank in range(world):
         got = out[(world, rank)]
         for key, tr in (("d", False), ("a", True)):
@@ -605,3 +615,4 @@ def test_config5_four_ranks_vs_oracle(gpu):
             assert np.max(np.abs(sign * a - b)) <= 1e-9 * scale, rank
         ip = got["ip"]
         assert abs(abs(ip) - 1.0) < 0.5   # <a, d> before the rescaling: O(1)
+        assert abs(got["norm_grad"] - ng_ref) <= 1e-8 * ng_ref, (rank, got["norm_grad"], ng_ref)   # modes agree to 1e-9
