@@ -208,7 +208,10 @@ def write_fld(path: str, f: FldFile) -> None:
     try:
         with open(tmp, "wb") as fh:
             for p in parts:
-                fh.write(memoryview(p).cast("B") if isinstance(p, np.ndarray) else p)
+                if not isinstance(p, np.ndarray):
+                    fh.write(p)
+                elif p.size:   # an empty shard (more ranks than elements) writes header + tag only
+                    fh.write(memoryview(p).cast("B"))
         os.replace(tmp, path)
     except BaseException:
         with contextlib.suppress(OSError):

@@ -227,3 +227,24 @@ def test_read_fld_set_refuses_incomplete_and_foreign_sets(tmp_path):
     fld.write_fld(os.path.join(d3, fld.fld_name("KRY", "s", 0, 1)), f)
     with pytest.raises(ValueError, match="in no file"):
         fld.read_fld_set(d3, "KRY", "s", 1, lay=g.shard(1, 2))
+
+
+def test_sets_with_empty_shards(tmp_path):
+    """More ranks than elements: the writers of empty shards write element-less members (Nek5000
+    would too), and readers of any world size, empty shards included, get their elements back."""
+    sys.path.insert(0, ROOT)
+    from nekstab_next_amd import fld
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import cylinder_layout
+
+    g = cylinder_layout(3)
+    d = str(tmp_path)
+    for r in range(5):
+        lay = g.shard(r, 5)
+        fld.write_fld(os.path.join(d, fld.fld_name("KRY", "s", r, 1)), fld.fld_from_vector(lay, syn.hash_vector(lay, 7)))
+    for w in (1, 2, 5, 7):
+        for r in range(w):
+            lay = g.shard(r, w)
+            files = fld.read_fld_set(d, "KRY", "s", 1, lay=lay)
+            assert all(f.emap.size for f in files) and (lay.nelv > 0) == bool(files)
+            np.testing.assert_allclose(fld.vector_from_fld(lay, files), syn.hash_vector(lay, 7), rtol=0, atol=1e-13)
