@@ -130,7 +130,7 @@ def read_restart_hes(comm, directory: str, session: str, mstart: int, k_dim: int
     if comm.rank == 0:
         try:
             H = read_hes(os.path.join(directory, f"HES{session}{mstart:04d}"), mstart, k_dim)
-        except (OSError, ValueError) as e:
+        except Exception as e:  # noqa: BLE001 - flagged to every rank, raised on all of them
             err = e
     if comm.world > 1:
         t = torch.zeros(H.size + 1, dtype=torch.float64, device=device)

@@ -325,7 +325,7 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
             return FileNotFoundError(path(0))
         try:
             h = read_fld_header(path(0))
-        except (OSError, ValueError) as e:
+        except Exception as e:  # noqa: BLE001 - sent to every rank and raised there (no rank left waiting)
             return e
         if h.nfileo < 1:
             return ValueError(f"{path(0)}: nfileo={h.nfileo}")
