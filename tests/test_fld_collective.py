@@ -248,3 +248,38 @@ def test_sets_with_empty_shards(tmp_path):
             files = fld.read_fld_set(d, "KRY", "s", 1, lay=lay)
             assert all(f.emap.size for f in files) and (lay.nelv > 0) == bool(files)
             np.testing.assert_allclose(fld.vector_from_fld(lay, files), syn.hash_vector(lay, 7), rtol=0, atol=1e-13)
+
+
+def test_rank_local_reads_any_world_pair(tmp_path):
+    """Sets written by W ranks read by R ranks (random E, W, R, including W > E and R > E): every
+    reader gets exactly its elements and opens only the files whose element range meets its own."""
+    sys.path.insert(0, ROOT)
+    from nekstab_next_amd import fld
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.layout import cylinder_layout
+
+    rng = np.random.default_rng(11)
+    for case in range(12):
+        E, W, R = int(rng.integers(1, 30)), int(rng.integers(1, 9)), int(rng.integers(1, 9))
+        g = cylinder_layout(E)
+        d = str(tmp_path / f"c{case}")
+        os.makedirs(d)
+        for r in range(W):
+            lay = g.shard(r, W)
+            fld.write_fld(os.path.join(d, fld.fld_name("KRY", "s", r, 3)),
+                          fld.fld_from_vector(lay, syn.hash_vector(lay, case)))
+        opened = []
+        real = fld.read_fld
+        fld.read_fld = lambda p: (opened.append(p), real(p))[1]
+        try:
+            for r in range(R):
+                lay = g.shard(r, R)
+                opened.clear()
+                got = fld.vector_from_fld(lay, fld.read_fld_set(d, "KRY", "s", 3, lay=lay))
+                np.testing.assert_allclose(got, syn.hash_vector(lay, case), rtol=0, atol=1e-13)
+                e0, e1 = lay.elem_range()
+                need = {fid for fid in range(W) if g.shard(fid, W).elem_range()[0] < e1
+                        and g.shard(fid, W).elem_range()[1] > e0}
+                assert {int(os.path.basename(p).split(".")[0][len("KRYs"):]) for p in opened} == need, (E, W, R, r)
+        finally:
+            fld.read_fld = real
