@@ -118,33 +118,21 @@ class ArnoldiCheckpoint:
                 write_hes(os.path.join(self.dir, f"HES{self.session}{k:04d}"), H, k)
 
 
-def read_restart_hes(comm, directory: str, session: str, mstart: int, k_dim: int, device=None) -> np.ndarray:
+def read_restart_hes(comm, directory: str, session: str, mstart: int, k_dim: int) -> np.ndarray:
     """H for a restart at ``mstart``: rank 0 parses ``HES<session><mstart>`` and broadcasts the
     (k_dim+1) x k_dim matrix to every rank (eigensolvers.f90:244-266: ``if (nid == 0)`` read, then
-    ``bcast(H, (k_dim+1)*k_dim*wdsize)``).  A parse error on rank 0 is broadcast too (a NaN flag),
-    so every rank raises instead of waiting at the broadcast."""
-    import torch
-
-    H = np.zeros((k_dim + 1, k_dim), order="F")
-    err = None
+    ``bcast(H, (k_dim+1)*k_dim*wdsize)``).  A failure on rank 0 is broadcast in its place, so every
+    rank raises the same exception instead of waiting at the broadcast."""
+    got = None
     if comm.rank == 0:
         try:
-            H = read_hes(os.path.join(directory, f"HES{session}{mstart:04d}"), mstart, k_dim)
-        except Exception as e:  # noqa: BLE001 - flagged to every rank, raised on all of them
-            err = e
-    if comm.world > 1:
-        t = torch.zeros(H.size + 1, dtype=torch.float64, device=device)
-        if comm.rank == 0:
-            t[:-1] = torch.as_tensor(H.ravel(order="F"))
-            t[-1] = 1.0 if err is None else float("nan")
-        comm.broadcast_(t, src=0)
-        host = t.cpu().numpy()
-        if not np.isfinite(host[-1]):
-            raise err if err is not None else ValueError(f"rank 0 could not read HES{session}{mstart:04d}")
-        H = np.asfortranarray(host[:-1].reshape((k_dim + 1, k_dim), order="F"))
-    elif err is not None:
-        raise err
-    return H
+            got = read_hes(os.path.join(directory, f"HES{session}{mstart:04d}"), mstart, k_dim)
+        except Exception as e:  # noqa: BLE001 - sent to every rank, raised on all of them
+            got = e
+    got = comm.bcast_object(got, src=0)
+    if isinstance(got, BaseException):
+        raise got
+    return np.asfortranarray(got)
 
 
 def restart_vectors(lay, directory: str, session: str, mstart: int, comm=None):
@@ -158,7 +146,7 @@ def restart_vectors(lay, directory: str, session: str, mstart: int, comm=None):
 def load_restart(ctx: NekContext, directory: str, session: str, mstart: int, k_dim: int):
     """(Q, H) for ``krylov_schur(..., Q=Q, start=(mstart, H))``: Q[0:mstart+1] = KRY 1..mstart+1,
     H read on rank 0 and broadcast."""
-    H = read_restart_hes(ctx.comm, directory, session, mstart, k_dim, device=ctx.device)
+    H = read_restart_hes(ctx.comm, directory, session, mstart, k_dim)
     Q = ctx.basis(k_dim + 1)
     for i, v in enumerate(restart_vectors(ctx.layout, directory, session, mstart, ctx.comm)):
         Q[i].from_packed(v)

@@ -106,16 +106,10 @@ class Comm:
         dist.all_gather_object(out, me, group=self.group)
         return out
 
-    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        """In-place broadcast from ``src`` (the reference's ``bcast``, e.g. the restart H at
-        eigensolvers.f90:266)."""
-        if self.world > 1:
-            dist.broadcast(t, src=src, group=self.group)
-        return t
-
     def bcast_object(self, obj, src: int = 0):
-        """A picklable host object from ``src`` to every rank (setup-only messages: a file
-        header, an error to raise everywhere)."""
+        """A picklable host object from ``src`` to every rank — the reference's ``bcast`` of
+        setup-time data (the restart H, eigensolvers.f90:266; a field-file set's header), or an
+        error to raise on every rank."""
         if self.world == 1:
             return obj
         box = [obj]

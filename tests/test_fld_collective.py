@@ -283,3 +283,39 @@ def test_rank_local_reads_any_world_pair(tmp_path):
                 assert {int(os.path.basename(p).split(".")[0][len("KRYs"):]) for p in opened} == need, (E, W, R, r)
         finally:
             fld.read_fld = real
+
+
+def _missing_worker(rank, world, port, directory, out):
+    _init(rank, world, port)
+    try:
+        from nekstab_next_amd import checkpoint as ck
+        from nekstab_next_amd import fld
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.layout import cylinder_layout
+
+        comm = Comm()
+        res = []
+        try:
+            ck.read_restart_hes(comm, directory, "none", 3, 8)
+            res.append("read")
+        except FileNotFoundError:
+            res.append("hes missing")
+        try:
+            fld.read_fld_set(directory, "KRY", "none", 1, lay=cylinder_layout(9).shard(rank, world), comm=comm)
+            res.append("read")
+        except FileNotFoundError:
+            res.append("set missing")
+        comm.barrier()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_missing_files_raise_on_every_rank(tmp_path):
+    """A restart from files that are not there: rank 0's failure to parse HES, and the missing set
+    header, are broadcast, so every rank raises FileNotFoundError instead of waiting for rank 0."""
+    world = 3
+    out = mp.Manager().dict()
+    mp.spawn(_missing_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r] == ["hes missing", "set missing"], out[r]
