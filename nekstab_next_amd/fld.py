@@ -316,7 +316,8 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
     written with another distribution (a foreign writer) falls back to reading every header.
 
     Raises FileNotFoundError when fid 0 or any member fid < nfileo is missing (on every rank), and
-    ValueError when the files read do not cover the shard's elements — never a partial vector."""
+    ValueError when the files read do not cover the shard's elements — never a partial vector.  A
+    rank without elements gets one element-less FldFile carrying the set's header (time, istep)."""
     def path(fid):
         return os.path.join(directory, fld_name(prefix, session, fid, num))
 
@@ -329,7 +330,8 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
             return e
         if h.nfileo < 1:
             return ValueError(f"{path(0)}: nfileo={h.nfileo}")
-        return h.nfileo, h.nelgt
+        h.emap = np.zeros(0, dtype=np.int32)   # the set's header facts only (time, istep, sizes)
+        return h
 
     if comm is not None and comm.world > 1:
         hdr = comm.bcast_object(set_header() if comm.rank == 0 else None, src=0)
@@ -337,7 +339,7 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
         hdr = set_header()
     if isinstance(hdr, BaseException):
         raise hdr
-    n, nelgt = hdr
+    n, nelgt = hdr.nfileo, hdr.nelgt
     missing = [i for i in range(n) if not os.path.exists(path(i))]
     if missing:
         raise FileNotFoundError(f"{path(missing[0])} (set of {n} files, missing fids {missing})")
@@ -368,4 +370,6 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
     if not covered.all():
         raise ValueError(f"{prefix}{session}*.f{num:05d}: {int((~covered).sum())} of this rank's "
                          f"{e1 - e0} elements are in no file of the set")
-    return files
+    # a rank without elements gets the set's header (time, istep) with no elements, as load_fld
+    # sets time on every rank
+    return files or [hdr]
