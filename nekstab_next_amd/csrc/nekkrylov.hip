@@ -3454,6 +3454,7 @@ __global__ __launch_bounds__(kThreads) void k_symmetric_seed(int64_t n, const do
 int nkv_symmetric_seed(const nkv_layout* L, const double* ym, const double* zm, double alpha, double* qx,
                        double* qz, double* qt, void* stream) {
     CHECK(check_layout(L));
+    if (L->n_v == 0) return NKV_OK;   // an empty shard (more ranks than elements): nothing to touch
     CHECK(check_ptr(ym, "ym"));
     CHECK(check_ptr(zm, "zm"));
     CHECK(check_ptr(qx, "qx"));
@@ -3470,6 +3471,7 @@ int nkv_mth_rand_add(const nkv_layout* L, int lx1, int ly1, int lz1, int64_t e_f
                      const double* ym, const double* zm, double fc1, double fc2, double fc3, double* q,
                      void* stream) {
     CHECK(check_layout(L));
+    if (L->n_v == 0) return NKV_OK;   // an empty shard (more ranks than elements): nothing to touch
     if (lx1 < 1 || ly1 < 1 || lz1 < 1 || L->n_v % ((int64_t)lx1 * ly1 * lz1) != 0)
         return fail(NKV_EINVAL, "mth_rand: lx1*ly1*lz1=%d*%d*%d does not divide n_v=%lld", lx1, ly1, lz1,
                     (long long)L->n_v);
@@ -3497,6 +3499,7 @@ int nkv_group_average(int64_t n_groups, const int64_t* start, const int64_t* mem
 int nkv_wavemaker(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe, const double* aIm,
                   double* out, int ncomp, void* stream) {
     CHECK(check_layout(L));
+    if (L->n_v == 0) return NKV_OK;   // an empty shard (more ranks than elements): nothing to touch
     CHECK(check_ptr(dRe, "dRe"));
     CHECK(check_ptr(dIm, "dIm"));
     CHECK(check_ptr(aRe, "aRe"));
@@ -3515,6 +3518,7 @@ int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const do
                const double* zm, const double* u, int nfld, int64_t u_stride, double* grad, int64_t g_stride,
                void* stream) {
     CHECK(check_layout(L));
+    if (L->n_v == 0) return NKV_OK;   // an empty shard (more ranks than elements): nothing to touch
     if (ldim != 2 && ldim != 3) return fail(NKV_EINVAL, "gradm1: ldim=%d must be 2 or 3", ldim);
     if (lx1 < 2 || lx1 > 10) return fail(NKV_EINVAL, "gradm1: lx1=%d outside 2..10", lx1);
     const int pts = ldim == 3 ? lx1 * lx1 * lx1 : lx1 * lx1;
@@ -3531,7 +3535,6 @@ int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const do
     CHECK(check_ptr(u, "u"));
     CHECK(check_ptr(grad, "grad"));
     const int64_t nel = L->n_v / pts;
-    if (nel == 0) return NKV_OK;
 #define NKV_GRADM1_CASE(NX)                                                                                   \
     case NX:                                                                                                  \
         if (ldim == 3) launch_gradm1<3, NX>(nel, nfld, D, xm, ym, zm, u, u_stride, grad, g_stride, stream);  \
@@ -3556,6 +3559,7 @@ int nkv_gradm1(const nkv_layout* L, int lx1, int ldim, const double* D, const do
 int nkv_bf_sensitivity(const nkv_layout* L, const double* dRe, const double* dIm, const double* aRe,
                        const double* aIm, const double* grad, double* out, int ncomp, void* stream) {
     CHECK(check_layout(L));
+    if (L->n_v == 0) return NKV_OK;   // an empty shard (more ranks than elements): nothing to touch
     CHECK(check_ptr(dRe, "dRe"));
     CHECK(check_ptr(dIm, "dIm"));
     CHECK(check_ptr(aRe, "aRe"));
@@ -3564,7 +3568,6 @@ int nkv_bf_sensitivity(const nkv_layout* L, const double* dRe, const double* dIm
     CHECK(check_ptr(out, "out"));
     if (ncomp < 2 || ncomp > 3 || ncomp > L->n_wf)
         return fail(NKV_EINVAL, "bf_sensitivity: ncomp=%d must be 2 or 3 and <= n_wf=%d", ncomp, L->n_wf);
-    if (L->n_v == 0) return NKV_OK;
     auto kern = ncomp == 3 ? k_bf_sensitivity<3> : k_bf_sensitivity<2>;
     hipLaunchKernelGGL(kern, dim3(grid_for(L->n_v)), dim3(kThreads), 0, S(stream), L->n_v, L->sv, dRe, dIm, aRe, aIm,
                        grad, out);

@@ -221,3 +221,29 @@ def test_explicit_reference_order_kept_for_nonorthonormal_bases():
     assert _nonorth_of("mgs2", cfg) == "mgs2" and _nonorth_of("mgs2-native", cfg) == "mgs2-native"
     assert _nonorth_of("dcgs2", cfg) == "mgs2-icwy" and _nonorth_of("dcgs2-native", cfg) == "mgs2-icwy-native"
     assert _nonorth_of("cgs2", KrylovSchurConfig(nonorth_mode="mgs2")) in _MGS2
+
+
+def test_segment_entry_points_are_noops_on_an_empty_shard():
+    """More ranks than elements: a rank's segment-only arrays (the wave-maker's and bf_sensitivity's
+    outputs, gradients, seed fields) are empty tensors whose data pointer is NULL.  Those entry
+    points return OK on an empty shard before any pointer check or launch (no device is touched,
+    so this runs on the CPU) and still reject a NULL pointer on a non-empty one."""
+    import ctypes
+
+    from nekstab_next_amd import _lib
+    from nekstab_next_amd.layout import cylinder_layout
+
+    from nekstab_next_amd.sensitivity import velocity_layout
+
+    lib = _lib.load()
+    lay = velocity_layout(cylinder_layout(2)).shard(0, 3)
+    assert lay.n_v == 0 and lay.sv == 0
+    L = ctypes.byref(lay.c_struct())
+    assert lib.nkv_wavemaker(L, None, None, None, None, None, 2, None) == 0
+    assert lib.nkv_gradm1(L, lay.lx1, 2, None, None, None, None, None, 2, 0, None, 0, None) == 0
+    assert lib.nkv_bf_sensitivity(L, None, None, None, None, None, None, 2, None) == 0
+    assert lib.nkv_mth_rand_add(L, lay.lx1, lay.lx1, 1, 0, None, None, None, 1.0, 1.0, 1.0, None, None) == 0
+    assert lib.nkv_symmetric_seed(L, None, None, 1.0, None, None, None, None) == 0
+    full = velocity_layout(cylinder_layout(2))
+    assert lib.nkv_wavemaker(ctypes.byref(full.c_struct()), None, None, None, None, None, 2, None) != 0
+    assert "NULL" in _lib.last_error()
