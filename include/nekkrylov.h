@@ -382,6 +382,10 @@ int nkv_op_cdiag(const nkv_layout* L, const double* cr, const double* ci, const 
                  void* stream);
 
 /* ---- sensitivity post-processing (sensitivity.f90) ---------------------------------------
+ * These entry points and the two seed kernels below work on field segments only (no time slot):
+ * on an empty shard (n_v = 0, a rank without elements) they return NKV_OK without reading any
+ * pointer, since its segment arrays are empty (NULL).
+ *
  * wave_maker's pointwise product (sensitivity.f90:69-71), after biorthogonalize (:63-66):
  *   out[i] = sqrt(sum_c dRe_c[i]^2 + dIm_c[i]^2) * sqrt(sum_c aRe_c[i]^2 + aIm_c[i]^2),
  * c over the first ncomp (2 or 3, <= n_wf) weighted fields — the velocity components — summed in
