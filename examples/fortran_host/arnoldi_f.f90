@@ -47,7 +47,7 @@ program arnoldi_f
    L%sv = ((L%n_v + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
    L%sp = ((L%n_p + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
    L%ld = ((L%n_wf*L%sv + L%sp + 1 + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
-   if (nkv_abi_version() /= 1) stop 'ABI mismatch'
+   if (nkv_abi_version() /= 2) stop 'ABI mismatch'
 
    vbytes = int(L%ld, c_size_t)*8
    call ck(hipMalloc(Q, (m + 1)*vbytes), 'hipMalloc Q')

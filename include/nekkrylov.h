@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define NKV_ABI_VERSION 1
+#define NKV_ABI_VERSION 2   /* 2 (round 5): the opt-in deferred-basis DCGS2 entry points removed; rotation limited by kept columns */
 
 /* Rows per tile: fields are padded to a multiple of this many doubles. */
 #define NKV_TILE 4096
@@ -56,10 +56,11 @@ extern "C" {
  * live in LDS (64 B per column for the two-vector dot).  The reference's k_dim defaults to 100
  * (main.f90:9); GMRES on the cylinder uses 200 (1cyl.usr:14). */
 #define NKV_MAX_COLS 1024
-/* Most input columns of one basis rotation (nkv_rotate / nkv_rotate_cols with more than 16 output
- * columns): a Krylov–Schur restart keeping more than 16 vectors and the materialisation of a lazy
- * DCGS2 basis, so those need k_dim <= 576. */
-#define NKV_ROT_MAX_K 576
+/* Most output columns of one basis rotation (nkv_rotate / nkv_rotate_cols): every output column is
+ * held in registers while the k input columns stream past (no k-sized state, so any k up to
+ * NKV_MAX_COLS).  A Krylov–Schur restart keeps mstart-1 < k_dim columns; the reference's k_dim is
+ * at most 200 (1cyl.usr:14), so 256 covers every restart of k_dim <= 257. */
+#define NKV_ROT_MAX_OUT 256
 
 /* Status codes (every entry point). */
 #define NKV_OK 0
@@ -333,35 +334,17 @@ int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, i
                               int64_t ldh, double* f, double* scratch_dev, void* ws, nkv_matvec_fn matvec,
                               void* mv_user, nkv_allreduce_fn allreduce, void* ar_user, unsigned flags, void* stream);
 
-/* DCGS2 over a LAZY basis (same replacement target): the finished q_j is never written.  The stored
- * columns S_0..S_{m-1} keep the raw provisional vectors and the orthonormal basis is Q = S T with
- * T upper triangular (device, column c at T + c*ldt, ldt >= m+1; T_0 empty, a finished column's
- * T column = e_c).  Step j (m = j-1; S column m holds u; f = A u):
- *   nkv_block_dot2(S, j, x=u, y=f) -> h                                            (all-reduce 2j)
- *   nkv_dcgs2_coef_lazy(m, h, h+j, nrm, H, ldh, coef, T, ldt)   as nkv_dcgs2_coef after mapping the
- *       raw dots by T_m^T; appends T column m; coef + 3m+5 = z (m+1 entries)
- *   nkv_dcgs2_update_lazy(S, m, coef, f, S col j) -> S col j = (A u) s/r - S[:,0:m+1] z  (the next u)
- * After the last step: nkv_block_dot(S, m+1, u) -> h, nkv_dcgs2_coef_lazy(m, h, NULL, h+m, ..., T),
- * nkv_block_update(S, m, coef+3m+5, u), nkv_normalize_dev(u, coef+2m+3): column m final, T column
- * m = e_m.  One output vector per update instead of two (8N bytes less per step); consumers fold T
- * into their coefficients (restart rotation V -> T V, mode reconstruction y -> T y) or rotate the
- * basis by T once (nkv_rotate_cols(S, L, T, ldt, L)). */
-int nkv_dcgs2_coef_lazy(int m, const double* hq_dev, const double* hw_dev, const double* nrm_prev_dev,
-                        double* H_dev, int64_t ldh, double* coef_dev, double* T_dev, int64_t ldt, void* ws,
-                        void* stream);
-int nkv_dcgs2_update_lazy(const nkv_layout* L, const double* S, int m, const double* coef_dev, const double* win,
-                          double* fout, void* ws, unsigned flags, void* stream);
-
 /* ---- Krylov–Schur restart (a10, schur_condensation eigensolvers.f90:421-442) --------------
  * In place: Q[:,0:k] <- Q[:,0:k] * V, V k-by-k column-major (leading dim ldv) in device memory.
- * The time slot is not rotated (the reference copies vx..t only, :421-432). k <= 576. */
+ * The time slot is not rotated (the reference copies vx..t only, :421-432).  k <= NKV_ROT_MAX_OUT
+ * (NKV_ESHAPE beyond). */
 int nkv_rotate(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, void* stream);
 
 /* Partial restart rotation, in place: Q[:,0:n_out] <- Q[:,0:k] * V[:,0:n_out], 1 <= n_out <= k.
  * Columns n_out..k-1 are left as they were.  schur_condensation only keeps the mstart selected
  * Schur vectors (eigensolvers.f90:416-459: Q(mstart+1..k) are overwritten by the next
  * factorisation before being read), so the restart calls this with n_out = mstart.
- * k <= NKV_ROT_MAX_K, or k <= NKV_MAX_COLS when n_out <= 16 (the usual restart). */
+ * k <= NKV_MAX_COLS, n_out <= NKV_ROT_MAX_OUT (NKV_ESHAPE beyond). */
 int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, int ldv, int n_out,
                     void* stream);
 

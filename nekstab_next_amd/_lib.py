@@ -17,9 +17,10 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see module d
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 
+NKV_ABI_VERSION = 2
 NKV_TILE = 4096
 NKV_MAX_COLS = 1024   # most columns per multi-dot (include/nekkrylov.h)
-NKV_ROT_MAX_K = 576   # most input columns per basis rotation (restart, lazy-basis materialisation)
+NKV_ROT_MAX_OUT = 256   # most output columns of a basis rotation with more than 16 kept (include/nekkrylov.h)
 NKV_OK, NKV_EINVAL, NKV_EHIP, NKV_ENAN, NKV_ESHAPE, NKV_ECALLBACK, NKV_EBREAKDOWN = 0, 1, 2, 3, 4, 5, 6
 NKV_TIME = 0x1
 NKV_ACCUMULATE = 0x2
@@ -101,8 +102,6 @@ _SIGNATURES = {
     "nkv_normalize_store": (c_int, [_L, _P, _P, _P, _P, c_uint, _P]),
     "nkv_mgs2_step": (c_int, [_L, _P, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_axpy_dot": (c_int, [_L, _P, _P, _P, _P, _P, _P, _P, c_uint, _P]),
-    "nkv_dcgs2_coef_lazy": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, c_int64, _P, _P]),
-    "nkv_dcgs2_update_lazy": (c_int, [_L, _P, c_int, _P, _P, _P, _P, c_uint, _P]),
     "nkv_rotate": (c_int, [_L, _P, c_int, _P, c_int, _P]),
     "nkv_rotate_cols": (c_int, [_L, _P, c_int, _P, c_int, c_int, _P]),
     "nkv_op_diag": (c_int, [_L, _P, _P, _P, c_double, _P]),
@@ -141,8 +140,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.nkv_abi_version() != 1:
-        raise ImportError(f"ABI mismatch: {path} reports {lib.nkv_abi_version()}, expected 1")
+    if lib.nkv_abi_version() != NKV_ABI_VERSION:
+        raise ImportError(f"ABI mismatch: {path} reports {lib.nkv_abi_version()}, expected {NKV_ABI_VERSION}")
     _lib = lib
     return lib
 

@@ -14,8 +14,7 @@ Two orthogonalisation modes share the rest of the path:
   ``h2 = Q^T W f`` in a single read of Q (+ all-reduce); ``f -= Q h2`` with the ||f||_W^2 partial
   fused (+ all-reduce); one kernel writing q_{k+1} = f/||f|| and the H column (h1 + h2, ||f||) on
   the device.  ~3jN streamed doubles per step instead of the reference's ~20jN, and 3
-  collectives instead of (2k+2)*n_fields.  ``"cgs2-unfused"`` runs the middle pass as two kernels
-  (4 reads of Q), kept for A/B measurement.
+  collectives instead of (2k+2)*n_fields.
 * ``"dcgs2"``: classical Gram–Schmidt with DELAYED re-orthogonalisation (low-synchronisation
   CGS2, cf. Świrydowicz et al. 2020, Bielich et al. 2022): step j projects A q_j once against the
   basis while re-orthogonalising the still-provisional q_j in the same pass — one two-vector
@@ -115,7 +114,7 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         return
     tf = NKV_TIME if ctx.time_in_dot else 0
     h1, h2, nrm = ctx.h1[:j], ctx.h2[:j], ctx.scal[3:4]
-    if mode in ("cgs2", "cgs2-unfused"):
+    if mode == "cgs2":
         lay, tm = ctx.layout, ctx.timer
         # algorithmic bytes: a dot reads j weighted columns + f_w + w; an update
         # reads j full columns + f and writes f (+ w for the fused norm)
@@ -127,23 +126,13 @@ def orthonormalize(ctx: NekContext, Q: Basis, j: int, f: NekVector, out_ptr: int
         if tm:
             tm.end("block_dot", b_dot)
         ctx.comm.allreduce_(h1)
-        if mode == "cgs2":  # f -= Q h1 and h2 = Q^T W f in ONE pass over Q
-            if tm:
-                tm.begin("update_dot")
-            ctx.call("nkv_block_update_dot", w, Q.ptr, j, h1.data_ptr(), f.ptr, h2.data_ptr(), ws,
-                     NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
-            if tm:
-                tm.end("update_dot", b_upd + 8.0 * lay.n_v)
-        else:
-            if tm:
-                tm.begin("block_update")
-            ctx.call("nkv_block_update", w, Q.ptr, j, h1.data_ptr(), f.ptr, None, ws, NKV_TIME, st)
-            if tm:
-                tm.end("block_update", b_upd)
-                tm.begin("block_dot")
-            ctx.call("nkv_block_dot", w, Q.ptr, j, f.ptr, h2.data_ptr(), ws, tf, st)
-            if tm:
-                tm.end("block_dot", b_dot)
+        # f -= Q h1 and h2 = Q^T W f in ONE pass over Q
+        if tm:
+            tm.begin("update_dot")
+        ctx.call("nkv_block_update_dot", w, Q.ptr, j, h1.data_ptr(), f.ptr, h2.data_ptr(), ws,
+                 NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
+        if tm:
+            tm.end("update_dot", b_upd + 8.0 * lay.n_v)
         ctx.comm.allreduce_(h2)
         if tm:
             tm.begin("block_update")
@@ -232,55 +221,6 @@ def _dcgs2_close(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
     if tm:
         tm.begin("block_update")
     ctx.call("nkv_block_update", w, Q.ptr, m, h.data_ptr(), u, None, ws, NKV_TIME, st)
-    if tm:
-        tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
-    ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
-
-
-def _dcgs2_step_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVector, first: bool) -> None:
-    """``_dcgs2_step`` over a lazy basis (include/nekkrylov.h, nkv_dcgs2_coef_lazy): the stored
-    columns stay the raw provisional vectors, T gains column j-1, and the update writes only the
-    next u = (A u) s/r - S[:, 0:j] z — the finished q_j is never stored."""
-    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
-    lay, tm = ctx.layout, ctx.timer
-    tf = NKV_TIME if ctx.time_in_dot else 0
-    m = j - 1
-    h = ctx.hd[: 2 * j]
-    hp, cp = h.data_ptr(), ctx.coef.data_ptr()
-    u = Q.col_ptr(m)
-    if tm:
-        tm.begin("block_dot2")
-    ctx.call("nkv_block_dot2", w, Q.ptr, j, u, f.ptr, hp, ws, tf | NKV_X_IS_LAST, st)
-    if tm:
-        tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
-    ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef_lazy", m, hp, hp + 8 * j, None if first else hp + 8 * m, Hd.t.data_ptr(),
-                Hd.k + 1, cp, Q.T.data_ptr(), Q.k, ws, st)
-    if tm:
-        tm.begin("dcgs2_update")
-    ctx.call("nkv_dcgs2_update_lazy", Q.ptr, m, cp, f.ptr, Q.col_ptr(j), ws, NKV_TIME, st)
-    if tm:
-        tm.end("dcgs2_update", 8.0 * ((m + 1) * lay.N + 2 * lay.N))
-
-
-def _dcgs2_close_lazy(ctx: NekContext, Q: Basis, Hd: HessenbergDev, m: int) -> None:
-    """``_dcgs2_close`` over a lazy basis: column m becomes final (T column m = e_m)."""
-    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
-    lay, tm = ctx.layout, ctx.timer
-    tf = NKV_TIME if ctx.time_in_dot else 0
-    h, coef = ctx.hd[: m + 1], ctx.coef
-    u = Q.col_ptr(m)
-    if tm:
-        tm.begin("block_dot")
-    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, u, h.data_ptr(), ws, tf, st)
-    if tm:
-        tm.end("block_dot", 8.0 * ((m + 1) * lay.N_w + lay.N_w + lay.n_v))
-    ctx.comm.allreduce_(h)
-    ctx.call_nl("nkv_dcgs2_coef_lazy", m, h.data_ptr(), None, h.data_ptr() + 8 * m, Hd.t.data_ptr(), Hd.k + 1,
-                coef.data_ptr(), Q.T.data_ptr(), Q.k, ws, st)
-    if tm:
-        tm.begin("block_update")
-    ctx.call("nkv_block_update", w, Q.ptr, m, coef[3 * m + 5:].data_ptr(), u, None, ws, NKV_TIME, st)
     if tm:
         tm.end("block_update", 8.0 * (m * lay.N + 2 * lay.N))
     ctx.call("nkv_normalize_dev", u, coef[2 * m + 3:].data_ptr(), None, 0, st)
@@ -408,21 +348,9 @@ def _dcgs2_native(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergD
     _lib.check(rc, entry)
 
 
-def _settle_basis(Q: Basis, mstart: int, lazy: bool) -> None:
-    """Before a factorisation from ``mstart``: from 1 only the caller's seed column is read, so any
-    lazy state is stale (T = I); otherwise columns < mstart must be usable — final, or (lazy run)
-    raw with the seed column mstart-1 final — else the basis is materialised first."""
-    if mstart <= 1:
-        Q.reset_T()
-    elif Q.lazy > (mstart - 1 if lazy else 0):
-        Q.materialize()
-    elif Q.lazy == 0:
-        Q.reset_T()
-
-
 def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,
                           mend: int, f: NekVector | None = None, mode: str = "cgs2", transpose: bool = False,
-                          on_step=None, lazy: bool = False) -> None:
+                          on_step=None) -> None:
     """k-step Arnoldi from column ``mstart`` to ``mend`` (1-based, inclusive), as
     krylov_decomposition.f90:68-96: f = A q_mstep; orthonormalise; Q(mstep+1) = f.
 
@@ -431,11 +359,7 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     finish each column in its own step.  DCGS2 finishes column j-1 in step j, so its hook for
     mstep = j-1 runs right after step j (one step later than the reference's call at :84, with the
     same content), and the hook for mend after the closing pass; ``"dcgs2-native"`` with a hook
-    runs this Python-driven DCGS2.
-
-    ``lazy=True`` (``"dcgs2"`` only): the finished columns are left as Q = S T (see ``Basis``) —
-    one vector write less per step; on return ``Q.lazy = mend`` (column mend is final).  The
-    Krylov–Schur restart folds T into its rotation; other readers call ``Q.materialize()``."""
+    runs this Python-driven DCGS2."""
     if mend < mstart:
         return
     if Q.k < mend + 1:
@@ -443,17 +367,15 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     if f is None:
         f = ctx.vector()
     if mode == "dcgs2-native":   # the same DCGS2 sequence, orchestrated by the library (one ABI call)
-        if on_step is None and not lazy:
+        if on_step is None:
             if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
                 raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-            _settle_basis(Q, mstart, lazy=False)
             _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose)
             return
         mode = "dcgs2"
     if mode == "dcgs2" and on_step is not None:   # lagged hooks: column j-1 is final after step j
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-        _settle_basis(Q, mstart, lazy=False)
         for mstep in range(mstart, mend + 1):
             (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
             _dcgs2_step(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
@@ -466,15 +388,13 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         if on_step is None:
             if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
                 raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-            _settle_basis(Q, mstart, lazy=False)
-            _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
+                _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
                           flags=_lib.NKV_MGS_ICWY)
             return
         mode = "mgs2-icwy"
     if mode == "mgs2-icwy":
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-        _settle_basis(Q, mstart, lazy=False)
         G = _icwy_gram(ctx, Q, mstart)
         for mstep in range(mstart, mend + 1):
             (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
@@ -485,31 +405,17 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
     if mode in ("cgs2-native", "mgs2-native") and on_step is None:   # per-column modes, one ABI call
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-        _settle_basis(Q, mstart, lazy=False)
         _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
                       flags=_lib.NKV_MGS2 if mode == "mgs2-native" else 0)
         return
     if mode == "dcgs2" and on_step is None:
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-        if lazy and mend > _lib.NKV_ROT_MAX_K:   # a lazy basis this wide could not be materialised
-            lazy = False
-        if lazy:
-            _settle_basis(Q, mstart, lazy=True)
-            Q.mark_lazy(Q.lazy)
-            for mstep in range(mstart, mend + 1):
-                (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
-                _dcgs2_step_lazy(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
-            _dcgs2_close_lazy(ctx, Q, Hd, mend)
-            Q.mark_lazy(mend)
-            return
-        _settle_basis(Q, mstart, lazy=False)
         for mstep in range(mstart, mend + 1):
             (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
             _dcgs2_step(ctx, Q, Hd, mstep, f, first=(mstep == mstart))
         _dcgs2_close(ctx, Q, Hd, mend)
         return
-    _settle_basis(Q, mstart, lazy=False)
     if mode == "dcgs2":
         mode = "cgs2"
     for mstep in range(mstart, mend + 1):
@@ -532,9 +438,8 @@ class FactorizationGraph:
     ``usable()`` is False for it and callers fall back to eager launches."""
 
     def __init__(self, ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, f: NekVector,
-                 mode: str = "cgs2", lazy: bool = False):
+                 mode: str = "cgs2"):
         self.ctx, self.op, self.Q, self.Hd, self.f, self.mode = ctx, op, Q, Hd, f, mode
-        self.lazy = lazy and mode == "dcgs2"
         self.graphs = {}
 
     def usable(self) -> bool:
@@ -549,21 +454,14 @@ class FactorizationGraph:
             return
         key = (mstart, mend, transpose)
         Q = self.Q
-        lazy = self.lazy and mend <= _lib.NKV_ROT_MAX_K
-        _ = Q.T   # allocated before any capture
-        _settle_basis(Q, mstart, lazy)   # host-side basis state, settled outside the graph
         g = self.graphs.get(key)
         if g is None:
             timer, self.ctx.timer = self.ctx.timer, None
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.ctx.device)
-            lazy0 = Q.lazy
             with torch.cuda.graph(g):
                 arnoldi_factorization(self.ctx, self.op, Q, self.Hd, mstart, mend, f=self.f, mode=self.mode,
-                                      transpose=transpose, lazy=lazy)
-            Q.mark_lazy(lazy0)   # capture did not run anything
+                                      transpose=transpose)
             self.ctx.timer = timer
             self.graphs[key] = g
         g.replay()
-        if lazy:
-            Q.mark_lazy(mend)

@@ -12,7 +12,7 @@ class KrylovSchurConfig:
     schur_del: float = 0.1    # keep |lambda| >= 1 - schur_del at restarts (:12)
     maxmodes: int = 20        # max eigenmodes exported (:13)
     mode: str = "dcgs2"       # "dcgs2" (block CGS2, delayed re-orth.: 2 reads of Q per step, the MI355X
-    #                           hot path) | "cgs2" (3 reads) | "cgs2-unfused" | "mgs2" (reference order);
+    #                           hot path) | "cgs2" (3 reads) | "mgs2" (reference order);
     #                           | "mgs2-icwy" (MGS in inverse compact WY form, 3 reads);
     #                           "dcgs2-native" | "cgs2-native" | "mgs2-native": the same sequences driven
     #                           by the library's one-call entry points (bit-identical)
@@ -22,9 +22,6 @@ class KrylovSchurConfig:
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
     graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)
-    lazy_basis: bool = False       # dcgs2: leave finished columns as Q = S T (one vector write less per
-    #                                step; the restart folds T in, the result basis is materialised once;
-    #                                measured +0.3 % at N=1e8, m=128 -- DESIGN.md §6)
     nonorth_mode: str = "mgs2-icwy"   # Gram–Schmidt where the basis is not orthonormal (noise/load seed,
     #                                time in k_dot after a restart), which must be modified G-S as the
     #                                reference's: "mgs2-icwy" (inverse compact WY form, 3 reads of Q

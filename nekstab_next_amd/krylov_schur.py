@@ -112,16 +112,13 @@ def schur_condensation(ctx: NekContext, H: np.ndarray, Q: Basis, k: int, cfg: Kr
     if ms > 0:
         # Only Q(1:ms) survive the restart: Q(ms+1) <- Q(k+1) below and Q(ms+2..k) are rewritten by
         # the next factorisation before any read, so the device rotation writes ms columns
-        # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.  A lazy basis
-        # (Q = S T, see Basis) is rotated by T Z instead: the restart materialises it for free.
-        Zr = Q.fold(np.asfortranarray(Z[:, :ms]), k)
-        Zd = torch.as_tensor(np.asfortranarray(Zr).ravel(order="F")).to(ctx.device)
+        # (reads k): 8N(k+ms) bytes instead of the reference's full Q(:,1:k) Z.
+        Zd = torch.as_tensor(np.asfortranarray(Z[:, :ms]).ravel(order="F")).to(ctx.device)
         if ctx.timer:
             ctx.timer.begin("rotate")
         ctx.call("nkv_rotate_cols", Q.ptr, int(k), Zd.data_ptr(), int(k), int(ms), ctx.stream)
         if ctx.timer:
             ctx.timer.end("rotate", 8.0 * ctx.layout.N * (k + ms))
-    Q.reset_T()   # columns 0..ms-1 rotated (final); Q(k+1) is final
     H[ms, :] = b_vec @ Z
     mstart = ms + 1
     # Q(mstart) <- Q(k+1): nopcopy moves the fields only, not time (:458-459)
@@ -190,11 +187,10 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     schur_cnt = 0
     res = KrylovSchurResult(None, None, None, 0, 0, H, Q)
     hook = None if on_step is None else (lambda mstep: on_step(mstep, Q, Hd))
-    lazy = cfg.lazy_basis and cfg.mode == "dcgs2" and hook is None
     if cfg.graphs and ctx.comm.world > 1:
         raise ValueError("KrylovSchurConfig.graphs=True is refused at world size > 1: HIP-graph capture of "
                          "the RCCL all-reduces has not been validated on more than one GPU; run eagerly")
-    graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode, lazy) if (cfg.graphs and hook is None) else None
+    graphs = FactorizationGraph(ctx, op, Q, Hd, f, cfg.mode) if (cfg.graphs and hook is None) else None
     if graphs is not None and not graphs.usable():
         graphs = None
     # the "noise" seed leaves Q(1) unnormalised (eigensolvers.f90:195-203); the reference's MGS2
@@ -206,7 +202,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # it too: its checkpointed basis descends from the same Q(1) (pass the original seed_mode).
     mode = _nonorth_of(cfg.mode, cfg) if cfg.seed_mode in ("noise", "load", "symm") else cfg.mode
     if mode != cfg.mode:
-        graphs, lazy = None, False
+        graphs = None
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)
     while True:
         if mode not in _MGS2:
@@ -219,7 +215,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
                 graphs.run(mstart, k, transpose)
             else:
                 arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose,
-                                      on_step=hook, lazy=lazy)
+                                      on_step=hook)
             H[...] = Hd.download()  # columns mstart..k written on the device, the rest as uploaded
             ctx.check_nan()
         except NkvNaNError:
@@ -235,11 +231,10 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
                 # invariant subspace reached: redo this factorisation from its starting state in the
                 # reference's MGS2 order, and keep that order for the rest of the solve
                 res.breakdowns.append(mstart)
-                Q.reset_T()   # a lazy factorisation leaves Q = S T from Q(mstart) on; T was I before
                 Q.storage[mstart - 1].copy_(snap.storage)
                 H[...] = H_before
                 Hd.upload(H)
-                mode, graphs, lazy = _mgs2_of(mode), None, False
+                mode, graphs = _mgs2_of(mode), None
                 arnoldi_factorization(ctx, op, Q, Hd, mstart, k, f=f, mode=mode, transpose=transpose,
                                       on_step=hook)
                 H[...] = Hd.download()
@@ -256,13 +251,12 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
             # the restart moves the fields but not `time` (eigensolvers.f90:421-432, 458-459), so
             # with time in k_dot (uparam(1)==2.1) the kept basis is no longer orthonormal: from here
             # on modified Gram–Schmidt is mirrored (CGS2/DCGS2 assume an orthonormal basis)
-            mode, graphs, lazy = _nonorth_of(mode, cfg), None, False
+            mode, graphs = _nonorth_of(mode, cfg), None
         res.mstart_history.append(mstart)
         res.selected_history.append(selected)
         Hd.upload(H)
         if on_restart is not None:
             on_restart(schur_cnt, mstart)
-    Q.materialize()   # the caller gets an orthonormal basis (one rotation per solve with a lazy basis)
     res.vals, res.vecs, res.residual, res.converged, res.schur_cnt = vals, vecs, residual, cnt, schur_cnt
     res.H = H
     return res
@@ -294,7 +288,6 @@ def orthonormality_report(ctx: NekContext, Q: Basis, k: int) -> np.ndarray:
     """Gram matrix G[i, j] = <q_i, q_j>_W (k_dot, no time term) of Q[0:k] — the self-check the
     reference writes to ``orthonormality.dat`` after the solve (eigensolvers.f90:335-345).  One
     multi-dot per column over the columns after it (upper triangle, k(k+1)/2 dots in k launches)."""
-    Q.materialize()
     G = np.zeros((k, k))
     h = ctx.h1
     for i in range(k):

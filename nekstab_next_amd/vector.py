@@ -75,7 +75,7 @@ class NekContext:
         self.scal = torch.zeros(8, **f64)
         # DCGS2: [Q^T W q_j ; Q^T W A q_j] (one all-reduce) and the small-step coefficients
         self.hd = torch.zeros(2 * (max_cols + 1), **f64)
-        self.coef = torch.zeros(4 * max_cols + 16, **f64)   # DCGS2: [x | c | 4 scalars | a | z (lazy)]
+        self.coef = torch.zeros(4 * max_cols + 16, **f64)   # DCGS2: [x | c | 4 scalars | a]
 
     # ---- plumbing ----------------------------------------------------------------------------
     @property
@@ -215,14 +215,7 @@ class ComplexNekVector:
 
 
 class Basis:
-    """``k`` vectors in ONE contiguous allocation at stride ``ld`` (column c = Q + c*ld).
-
-    Lazy columns: after a lazy DCGS2 factorisation (``arnoldi_factorization(..., lazy=True)``) the
-    first ``lazy`` stored columns S are the raw provisional vectors and the orthonormal basis is
-    Q[:, :lazy] = S[:, :lazy] T (T upper triangular, on the device, column c = ``T[c]``).  The
-    combinations (``combine``, ``k_matmul``) and the Krylov–Schur restart fold T into their
-    coefficients; ``materialize()`` rotates the stored columns by T once (anything that reads
-    columns as vectors must call it first)."""
+    """``k`` vectors in ONE contiguous allocation at stride ``ld`` (column c = Q + c*ld)."""
 
     def __init__(self, ctx: NekContext, k: int):
         self.ctx = ctx
@@ -230,55 +223,6 @@ class Basis:
         self.storage = torch.zeros((k, ctx.layout.ld), dtype=torch.float64, device=ctx.device)
         self._ptr = self.storage.data_ptr()          # the allocation never moves
         self._stride = ctx.layout.ld * 8
-        self.lazy = 0
-        self._T = None
-        self._T_identity = False
-
-    @property
-    def T(self) -> torch.Tensor:
-        """(k, k) device tensor, row c = column c of T (column-major T with leading dim k)."""
-        if self._T is None:
-            self._T = torch.zeros((self.k, self.k), dtype=torch.float64, device=self.ctx.device)
-            self._T.diagonal().fill_(1.0)
-            self._T_identity = True
-        return self._T
-
-    def reset_T(self) -> None:
-        """All columns final: T = I (no device work when it already is)."""
-        if self._T is not None and not self._T_identity:
-            self._T.zero_()
-            self._T.diagonal().fill_(1.0)
-        self._T_identity = True
-        self.lazy = 0
-
-    def mark_lazy(self, n: int) -> None:
-        self.lazy = int(n)
-        self._T_identity = False
-
-    def T_host(self, n: int) -> np.ndarray:
-        """T[:n, :n] as a numpy array (upper triangular)."""
-        return self.T[:n, :n].detach().cpu().numpy().T.copy()
-
-    def fold(self, y, k: int):
-        """Coefficients for the STORED columns equivalent to y on the first k final columns."""
-        L = min(self.lazy, int(k))
-        if L == 0:
-            return y
-        if isinstance(y, torch.Tensor):   # small: fold on the host (no device GEMM library)
-            out = y.detach().cpu().numpy().copy()
-            out[:L] = self.T_host(L) @ out[:L]
-            return torch.as_tensor(out).to(y.device)
-        out = np.array(y, dtype=np.float64, copy=True)
-        out[:L] = self.T_host(L) @ out[:L]
-        return out
-
-    def materialize(self) -> None:
-        """Q[:, :lazy] <- S[:, :lazy] T in place (one restart-style rotation), then T = I."""
-        L = self.lazy
-        if L > 0:
-            self.ctx.call("nkv_rotate_cols", self._ptr, int(L), self.T.data_ptr(), int(self.k), int(L),
-                          self.ctx.stream)
-        self.reset_T()
 
     @property
     def ptr(self) -> int:
@@ -354,7 +298,7 @@ def k_matmul(dq: NekVector, Q: Basis, y, k: int) -> None:
     streams the resident basis once (NKV_OVERWRITE block update)."""
     ctx = dq.ctx
     yd = ctx.h1[:k]
-    yd.copy_(torch.as_tensor(Q.fold(np.asarray(y, dtype=np.float64)[:k], k)).to(ctx.device))
+    yd.copy_(torch.as_tensor(np.asarray(y, dtype=np.float64)[:k]).to(ctx.device))
     ctx.call("nkv_block_update", _ptr(ctx.w), Q.ptr, int(k), _ptr(yd), dq.ptr, None, _ptr(ctx.ws),
              NKV_OVERWRITE | NKV_TIME, ctx.stream)
 
@@ -362,7 +306,6 @@ def k_matmul(dq: NekVector, Q: Basis, y, k: int) -> None:
 def combine(out: NekVector, Q: Basis, y: torch.Tensor, k: int, with_time: bool = True) -> None:
     """out = Q[:, :k] y with ``y`` already a device tensor (mode reconstruction, a19)."""
     ctx = out.ctx
-    y = Q.fold(y, k)
     ctx.call("nkv_block_update", _ptr(ctx.w), Q.ptr, int(k), _ptr(y), out.ptr, None, _ptr(ctx.ws),
              NKV_OVERWRITE | (NKV_TIME if with_time else 0), ctx.stream)
 

@@ -12,8 +12,12 @@ What it restates (each function cites the reference line it follows):
   ``ts_gmres``, ``biorthogonalize``, ``wave_maker``, ``bf_sensitivity`` (with Nek5000's
   ``gradm1``), the legacy ``matvec`` dispatcher,
   ``ts_steady_force_sensitivity``, ``newton_krylov``, the seed noise ``mth_rand`` with its
-  direct-stiffness averaging: this file, calling SciPy's LAPACK (OpenBLAS 0.3.28) for
-  dgeev / dgees / dtrsen / dgels with the reference's arguments and workspace sizes.
+  direct-stiffness averaging: this file, calling Intel MKL (``mkl_lapack.py``: the LAPACK the
+  reference's build links, bin/mks:32-44) for dgeev / dgees / dtrsen / dgels with the reference's
+  arguments and workspace sizes.  The product calls SciPy's OpenBLAS, so the dense half of every
+  product-vs-oracle check compares two independent LAPACK implementations.
+  ``NEKSTAB_ORACLE_LAPACK=openblas`` (or ``use_lapack("openblas")``) runs the oracle on SciPy's
+  OpenBLAS instead: the fixtures record both side by side (tests/golden/make_golden.py).
 
 Parity status: **parity unpinned** against reference outputs.  The reference ships no tests or
 golden vectors for this path, and its Fortran cannot be built here without
@@ -30,6 +34,8 @@ from ctypes import POINTER, Structure, c_double, c_int, c_int32, c_int64, c_uint
 
 import numpy as np
 from scipy.linalg import lapack as _lp
+
+import mkl_lapack as _mkl
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
@@ -224,11 +230,47 @@ def sort_eigendecomp(vals, vecs):
 
 # ---- dense steps (lapack_wrapper.f90) -----------------------------------------------------------
 
+_LAPACK = os.environ.get("NEKSTAB_ORACLE_LAPACK", "mkl").lower()
+if _LAPACK not in ("mkl", "openblas"):
+    raise ValueError(f"NEKSTAB_ORACLE_LAPACK={_LAPACK!r}: expected 'mkl' or 'openblas'")
+
+
+def lapack_name() -> str:
+    """The LAPACK the oracle's dense steps run on: ``"mkl"`` (default) or ``"openblas"``."""
+    return _LAPACK
+
+
+def use_lapack(name: str) -> str:
+    """Switch the oracle's LAPACK; returns the previous choice."""
+    global _LAPACK
+    name = name.lower()
+    if name not in ("mkl", "openblas"):
+        raise ValueError(name)
+    prev, _LAPACK = _LAPACK, name
+    return prev
+
+
+def lapack_version() -> str:
+    if _LAPACK == "mkl":
+        return _mkl.version()
+    import scipy
+
+    return f"SciPy {scipy.__version__} OpenBLAS"
+
+
+def _dgeev(A):
+    n = A.shape[0]
+    if _LAPACK == "mkl":
+        return _mkl.dgeev(A)
+    wr, wi, _, vr, info = _lp.dgeev(np.array(A, order="F", copy=True), compute_vl=0, compute_vr=1, lwork=4 * n)
+    return wr, wi, vr, info
+
+
 def eig(A):
     """lapack_wrapper.f90:114-177: dgeev('N','V', lwork=4n) on a copy, conjugate-pair assembly,
     sort_eigendecomp."""
     n = A.shape[0]
-    wr, wi, _, vr, info = _lp.dgeev(np.array(A, order="F", copy=True), compute_vl=0, compute_vr=1, lwork=4 * n)
+    wr, wi, vr, info = _dgeev(A)
     assert info == 0, info
     vecs = np.array(vr, dtype=np.complex128)
     i = 0
@@ -243,17 +285,26 @@ def eig(A):
 
 
 def schur_sorted(A):
-    """lapack_wrapper.f90:3-55: dgees('V','S', select_eigvals: sqrt(wr**2+wi**2) > 0.9, lwork=3n)."""
+    """lapack_wrapper.f90:3-55: dgees('V','S', select_eigvals: sqrt(wr**2+wi**2) > 0.9, lwork=3n).
+    ``info`` is ignored, as the reference does."""
     n = A.shape[0]
-    t, _, wr, wi, vs, _, info = _lp.dgees(lambda a, b: int(np.sqrt(a ** 2 + b ** 2) > 0.9),
-                                          np.array(A, order="F", copy=True), compute_v=1, sort_t=1, lwork=3 * n)
+    if _LAPACK == "mkl":
+        t, vs, wr, wi, _sdim, _info = _mkl.dgees(A)
+    else:
+        t, _, wr, wi, vs, _, _info = _lp.dgees(lambda a, b: int(np.sqrt(a ** 2 + b ** 2) > 0.9),
+                                               np.array(A, order="F", copy=True), compute_v=1, sort_t=1,
+                                               lwork=3 * n)
     return np.array(t, order="F"), np.array(vs, order="F"), wr + 1j * wi
 
 
 def ordschur(T, Z, selected):
     """lapack_wrapper.f90:59-111: dtrsen('N','V'), lwork=n, liwork=1."""
     n = T.shape[0]
-    ts, qs, _, _, m, _, _, info = _lp.dtrsen(selected.astype(np.int32), T, Z, job="N", wantq=1, lwork=n, liwork=1)
+    if _LAPACK == "mkl":
+        ts, qs, _m, info = _mkl.dtrsen(T, Z, selected)
+    else:
+        ts, qs, _, _, _m, _, _, info = _lp.dtrsen(selected.astype(np.int32), T, Z, job="N", wantq=1, lwork=n,
+                                                  liwork=1)
     assert info == 0, info
     return np.array(ts, order="F"), np.array(qs, order="F")
 
@@ -261,6 +312,9 @@ def ordschur(T, Z, selected):
 def lstsq(A, b):
     """lapack_wrapper.f90:248-300: dgels('N'), lwork=2mn; x = b_tilde(1:n)."""
     m, n = A.shape
+    if _LAPACK == "mkl":
+        x, _info = _mkl.dgels(A, b)
+        return x
     _, x, info = _lp.dgels(np.array(A, order="F", copy=True), np.array(b, copy=True), trans="N", lwork=2 * m * n)
     return np.array(x[:n])
 
@@ -319,7 +373,7 @@ def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, sc
         H[...] = H0
         Q[: ms + 1] = Qs[: ms + 1]
         mstart = ms + 1
-    hist = dict(mstart=[], cnt=[], selected=[], H_first=None)
+    hist = dict(mstart=[], cnt=[], selected=[], H_first=None, H_restart=[])
     while True:
         if on_step is None and stop_after is None:
             arnoldi_factorization(L, w, matvec, Q, H, mstart, k_dim)
@@ -339,6 +393,7 @@ def krylov_schur(L: OLayout, w, matvec, q1, k_dim, schur_tgt, eigen_tol=1e-6, sc
         if schur_tgt <= 0 or cnt >= schur_tgt or schur_cnt >= max_restarts:
             break
         schur_cnt += 1
+        hist["H_restart"].append(H.copy())   # the (k+1) x k matrix schur_condensation starts from
         mstart, sel = schur_condensation(L, H, Q, k_dim, schur_del, schur_tgt)
         hist["mstart"].append(mstart)
         hist["selected"].append(sel)

@@ -14,8 +14,11 @@ Provenance, per fixture:
   order), the seed of the config-2 golden run; lets the GPU box run on the reference's own data
   without ``/root/reference``.
 * ``ks_*.npz`` / ``gmres_*.npz`` — outputs of the CPU oracle (``oracle/``: the C restatement of
-  ``update_hessenberg_matrix`` and the numpy/SciPy-LAPACK restatement of the drivers) on the
-  synthetic BASELINE operators.  The reference's Fortran is not buildable in this image (DESIGN.md
+  ``update_hessenberg_matrix`` and the numpy restatement of the drivers) on the synthetic BASELINE
+  operators, with the dense steps on Intel MKL (``oracle/mkl_lapack.py``, the LAPACK the
+  reference's build links, bin/mks:32-44) as the primary keys and the same run on SciPy's OpenBLAS
+  (the product's LAPACK) as ``*_openblas`` keys; the Krylov–Schur ones also hold every restart's
+  input Hessenberg matrix (``H_restart``) and selected mask.  The reference's Fortran is not buildable in this image (DESIGN.md
   §3), so these are oracle outputs, not reference outputs: they freeze the oracle (a change to it
   shows up as a fixture mismatch) and let the GPU tests check the HIP path without running the
   oracle.  Parity against the reference itself stays "unpinned" (DESIGN.md §3).
@@ -25,11 +28,15 @@ Provenance, per fixture:
   ``bf_1cyl0_seed.npz``), the other three parts hashed (``synthetic.hash_vector`` seeds 41-43).
   Oracle output: freezes the restatement and lets the GPU test run the product's file chain
   against it without the oracle.
+* ``lapack_split.npz`` — the restart's dense chain (dgees sorted -> select_eigenvalues -> dtrsen)
+  under MKL on Hessenberg matrices built with ``ordering.npz``'s spectra, OpenBLAS's Schur order
+  beside it (``gen_lapack_split``).
 * ``ordering.npz`` — inputs/outputs of the C transliteration of ``quicksort2``
   (core/utils.f90:29-138), ``select_eigenvalues`` (core/eigensolvers.f90:688-754) and
   ``sort_eigendecomp`` (core/lapack_wrapper.f90:181-228), including the pivot defect.
 
 usage: python tests/golden/make_golden.py        (writes next to this file)
+       python tests/golden/make_golden.py --only-solvers   (the LAPACK-dependent fixtures only)
 """
 from __future__ import annotations
 
@@ -105,6 +112,42 @@ def _checksum(a):
     return np.array([np.sum(a), np.sum(a * a), a[0], a[-1]])
 
 
+def _stack_masks(masks, k):
+    return np.array(masks, dtype=bool).reshape(len(masks), k)
+
+
+def _both(fn):
+    """Run an oracle computation under MKL (the fixture's primary keys) and under SciPy's OpenBLAS
+    (the ``*_openblas`` keys): SURVEY §8(c), "record both in fixtures to detect ordering ties"."""
+    import oracle as orc
+
+    out = {}
+    prev = orc.lapack_name()
+    try:
+        for lp in ("mkl", "openblas"):
+            orc.use_lapack(lp)
+            out[lp] = fn()
+    finally:
+        orc.use_lapack(prev)
+    return out["mkl"], out["openblas"]
+
+
+def _ks_keys(rm, ro, k):
+    """Krylov–Schur fixture keys: MKL trajectory + the restart inputs (H before each
+    schur_condensation) + the OpenBLAS trajectory side by side."""
+    import oracle as orc
+
+    z = dict(vals=rm["vals"], residual=rm["residual"], mstart=np.array(rm["mstart"], dtype=np.int64),
+             cnt=np.array(rm["cnt"], dtype=np.int64), schur_cnt=rm["schur_cnt"], H_first=rm["H_first"],
+             selected=_stack_masks(rm["selected"], k),
+             H_restart=np.array(rm["H_restart"]).reshape(len(rm["H_restart"]), k + 1, k),
+             vals_openblas=ro["vals"], residual_openblas=ro["residual"],
+             mstart_openblas=np.array(ro["mstart"], dtype=np.int64), cnt_openblas=np.array(ro["cnt"], dtype=np.int64),
+             schur_cnt_openblas=ro["schur_cnt"], selected_openblas=_stack_masks(ro["selected"], k),
+             lapack=np.array(orc._mkl.version()))
+    return z
+
+
 def gen_solvers():
     import oracle as orc
     from helpers import olayout, oracle_diag_matvec, oracle_rot2_matvec
@@ -124,11 +167,9 @@ def gen_solvers():
     d, exact = syn.diag_spectrum(lay)
     dref = syn.to_reference_order(lay, d)
     q1 = seed_of(lay, L, w, 11)
-    r = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
-    np.savez(os.path.join(HERE, "ks_config1.npz"), vals=r["vals"], residual=r["residual"],
-             mstart=np.array(r["mstart"]), cnt=np.array(r["cnt"]), schur_cnt=r["schur_cnt"],
-             H_first=r["H_first"], H_final=r["H"], seed_checksum=_checksum(q1), d_checksum=_checksum(dref),
-             w_checksum=_checksum(w), exact=exact)
+    rm, ro = _both(lambda: orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5))
+    np.savez(os.path.join(HERE, "ks_config1.npz"), **_ks_keys(rm, ro, 16), H_final=rm["H"],
+             seed_checksum=_checksum(q1), d_checksum=_checksum(dref), w_checksum=_checksum(w), exact=exact)
 
     # config 2 on the real cylinder mesh (E=1996, N=175,648) seeded with the reference's own base
     # flow BF_1cyl0.f00001 (U, V, P); rotation-scaling operator, Krylov–Schur schur_tgt=2 (1cyl.usr:15)
@@ -136,16 +177,17 @@ def gen_solvers():
     lay = cylinder_layout(1996)
     L = olayout(lay)
     w = syn.mass_weights(lay)
-    f = fld.read_fld(os.path.join(REF, FLD_FILES[0]))
-    bf = syn.to_reference_order(lay, fld.vector_from_fld(lay, f))
-    np.savez_compressed(os.path.join(HERE, "bf_1cyl0_seed.npz"), seed_ref=bf)
+    if not os.path.exists(os.path.join(HERE, "bf_1cyl0_seed.npz")):   # frozen once written
+        f = fld.read_fld(os.path.join(REF, FLD_FILES[0]))
+        bf = syn.to_reference_order(lay, fld.vector_from_fld(lay, f))
+        np.savez_compressed(os.path.join(HERE, "bf_1cyl0_seed.npz"), seed_ref=bf)
+    bf = np.load(os.path.join(HERE, "bf_1cyl0_seed.npz"))["seed_ref"]
     q1 = orc.prepare_seed(L, w, bf)
     c, s, dr, exact = syn.rot2_operator(lay)
     for k in (16, 64):
-        r = orc.krylov_schur(L, w, oracle_rot2_matvec(lay, c, s, dr), q1, k, 2)
-        np.savez(os.path.join(HERE, f"ks_config2_bf_k{k}.npz"), vals=r["vals"], residual=r["residual"],
-                 mstart=np.array(r["mstart"], dtype=np.int64), cnt=np.array(r["cnt"]), schur_cnt=r["schur_cnt"],
-                 H_first=r["H_first"], seed_checksum=_checksum(q1), exact=exact)
+        rm, ro = _both(lambda: orc.krylov_schur(L, w, oracle_rot2_matvec(lay, c, s, dr), q1, k, 2))
+        np.savez(os.path.join(HERE, f"ks_config2_bf_k{k}.npz"), **_ks_keys(rm, ro, k),
+                 seed_checksum=_checksum(q1), exact=exact)
 
     # config 3 family, reduced (box3d E=40, N=90,592): plain 40-step Arnoldi on the shift-invert
     # Laplacian (|mu| from 0.1 to 3e8: the strongly graded spectrum of the headline config)
@@ -154,9 +196,25 @@ def gen_solvers():
     w = syn.mass_weights(lay)
     d, exact = syn.laplacian_shift_invert(lay)
     q1 = seed_of(lay, L, w, 11)
-    r = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 40, 0)
-    np.savez(os.path.join(HERE, "ks_config3_arnoldi.npz"), vals=r["vals"], residual=r["residual"],
-             H=r["H"], seed_checksum=_checksum(q1), exact=exact[:64])
+    rm, ro = _both(lambda: orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 40, 0))
+    np.savez(os.path.join(HERE, "ks_config3_arnoldi.npz"), vals=rm["vals"], residual=rm["residual"],
+             H=rm["H"], seed_checksum=_checksum(q1), exact=exact[:64], vals_openblas=ro["vals"],
+             residual_openblas=ro["residual"], lapack=np.array(orc.lapack_version()))
+
+    # config 3 layout (E=128, N=289,792) at BASELINE's m: a real k_dim=128 restart on a
+    # time-stepper-like clustered spectrum (one condensation keeping 25 columns), and the
+    # shift-invert family's Krylov–Schur at k_dim=32, schur_tgt=4 (converges without a restart)
+    lay = box3d_layout(128)
+    L = olayout(lay)
+    w = syn.mass_weights(lay)
+    q1 = seed_of(lay, L, w, 11)
+    d, exact = syn.clustered_spectrum(lay)
+    rm, ro = _both(lambda: orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 128, 4))
+    np.savez_compressed(os.path.join(HERE, "ks_restart_m128.npz"), **_ks_keys(rm, ro, 128),
+                        seed_checksum=_checksum(q1), exact=exact)
+    d, exact = syn.laplacian_shift_invert(lay)
+    rm, ro = _both(lambda: orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 32, 4))
+    np.savez(os.path.join(HERE, "ks_config3_k32.npz"), **_ks_keys(rm, ro, 32), exact=exact[:64])
 
     # config 4: ts_gmres on J = D - I (cylinder layout E=1996, the real mesh size), k_dim=200,
     # maxiter=10, tol=1e-9 (1cyl.usr:14, newton_krylov.f90:44, 1cyl.par:18,23)
@@ -171,11 +229,81 @@ def gen_solvers():
         y[:] = J * x
         y[-1] = 0.0
 
-    sol, hist = orc.ts_gmres(L, w, mv, rhs, maxiter=10, ksize=200, tol=1e-9)
+    (sol, hist), (sol_o, hist_o) = _both(lambda: orc.ts_gmres(L, w, mv, rhs, maxiter=10, ksize=200, tol=1e-9))
     np.savez(os.path.join(HERE, "gmres_config4.npz"), outer=np.array(hist["outer"]),
-             inner=np.array(hist["inner"]), y_last=hist["y"][-1], sol_checksum=_checksum(sol), sol_head=sol[:256], sol_wnorm2=orc.k_dot(L, w, sol, sol),
-             rhs_checksum=_checksum(rhs))
+             inner=np.array(hist["inner"]), y_last=hist["y"][-1], sol_checksum=_checksum(sol), sol_head=sol[:256],
+             sol_wnorm2=orc.k_dot(L, w, sol, sol), rhs_checksum=_checksum(rhs),
+             outer_openblas=np.array(hist_o["outer"]), inner_openblas=np.array(hist_o["inner"]),
+             y_last_openblas=hist_o["y"][-1], sol_head_openblas=sol_o[:256], lapack=np.array(orc.lapack_version()))
     orc.set_threads(1)
+
+
+def _spectrum_matrix(vals, rng):
+    """A real upper Hessenberg matrix with the given (conjugate-closed) spectrum: real 1x1 and
+    [[a, b], [-b, a]] 2x2 blocks, a random similarity (well conditioned), then a Householder
+    Hessenberg reduction — the shape of the k x k matrix a Krylov–Schur restart hands dgees."""
+    from scipy.linalg import hessenberg
+
+    n = vals.size
+    D = np.zeros((n, n))
+    used = np.zeros(n, dtype=bool)
+    i = 0
+    for j in range(n):
+        if used[j]:
+            continue
+        v = vals[j]
+        used[j] = True
+        if v.imag == 0:
+            D[i, i] = v.real
+            i += 1
+        else:
+            p = [q for q in range(n) if not used[q] and vals[q] == np.conj(v)][0]
+            used[p] = True
+            D[i:i + 2, i:i + 2] = [[v.real, abs(v.imag)], [-abs(v.imag), v.real]]
+            i += 2
+    S = np.eye(n) + 0.3 * rng.standard_normal((n, n)) / np.sqrt(n)
+    return hessenberg(S @ D @ np.linalg.inv(S))
+
+
+def gen_lapack_split():
+    """The restart's dense chain (dgees with the |lambda| > 0.9 sort -> select_eigenvalues ->
+    dtrsen) under MKL on matrices with the ordering fixture's spectra (real values, conjugate
+    pairs, zeros, values on both sides of 1 - schur_del and 0.9): per case the input matrix, MKL's
+    Schur-order eigenvalues, selected mask and count, and the reordered leading block's eigenvalues;
+    OpenBLAS's Schur-order eigenvalues beside them (to name where the two order differently)."""
+    import oracle as orc
+
+    z = np.load(os.path.join(HERE, "ordering.npz"))
+    rng = np.random.default_rng(505)
+    out = dict(n=[], A=[], vals_mkl=[], sel_mkl=[], cnt_mkl=[], lead_mkl=[], vals_openblas=[], args=[])
+    for n, v, (delta, nev) in zip(z["sel_len"], z["sel_vals"], z["sel_args"]):
+        A = _spectrum_matrix(v[:n], rng)
+        res = {}
+        for lp in ("mkl", "openblas"):
+            orc.use_lapack(lp)
+            T, Z, vals = orc.schur_sorted(A)
+            sel, cnt = orc.select_eigenvalues(vals, delta, int(nev))
+            T2, _ = orc.ordschur(T, Z, sel)
+            lead = np.linalg.eigvals(T2[:cnt, :cnt]) if cnt else np.zeros(0)
+            res[lp] = (vals, sel, cnt, lead)
+        orc.use_lapack("mkl")
+        out["n"].append(n)
+        out["A"].append(A)
+        out["vals_mkl"].append(res["mkl"][0])
+        out["sel_mkl"].append(res["mkl"][1])
+        out["cnt_mkl"].append(res["mkl"][2])
+        out["lead_mkl"].append(np.sort_complex(res["mkl"][3]))
+        out["vals_openblas"].append(res["openblas"][0])
+        out["args"].append((delta, nev))
+    nmax = max(out["n"])
+    padv = lambda xs, dt: np.array([np.pad(x, (0, nmax - len(x))) for x in xs], dtype=dt)  # noqa: E731
+    np.savez_compressed(
+        os.path.join(HERE, "lapack_split.npz"), n=np.array(out["n"]),
+        A=np.array([np.pad(a, ((0, nmax - a.shape[0]), (0, nmax - a.shape[0]))) for a in out["A"]]),
+        vals_mkl=padv(out["vals_mkl"], np.complex128), sel_mkl=padv(out["sel_mkl"], bool),
+        cnt_mkl=np.array(out["cnt_mkl"]), lead_mkl=padv(out["lead_mkl"], np.complex128),
+        vals_openblas=padv(out["vals_openblas"], np.complex128), args=np.array(out["args"]),
+        lapack=np.array(orc.lapack_version()))
 
 
 def wavemaker_inputs():
@@ -276,9 +404,14 @@ if __name__ == "__main__":
     if "--only-noise" in sys.argv:
         gen_noise()
         sys.exit(0)
+    if "--only-solvers" in sys.argv:   # the LAPACK-dependent fixtures (needs no /root/reference)
+        gen_solvers()
+        gen_lapack_split()
+        sys.exit(0)
     gen_fld()
     gen_ordering()
     gen_solvers()
+    gen_lapack_split()
     gen_wavemaker()
     gen_noise()
     for n in sorted(os.listdir(HERE)):

@@ -59,14 +59,15 @@ def test_bench_cpu_baseline_leg_small():
 
 def test_bench_cpu_baseline_measures_one_factorisation():
     """bench.cpu_baseline times one complete m-step factorisation (measured, not
-    extrapolated from single steps), reports both byte models and seconds to solution scaled to
-    N=1e8, and the round-3 fit (steps js only) with its error against the measured total."""
+    extrapolated from single steps), reports its value in the bytes the timed algorithm executes (the
+    GPU value's basis), seconds to solution scaled to N=1e8, and the round-3 fit
+    (steps js only) with its error against the measured total."""
     import bench
 
     r = bench.cpu_baseline(16, 16, 2, fit_js=(1, 4, 8, 16))
     assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
     assert r["seconds_per_factorisation_measured"] is True
-    assert r["value_reference_executed_gbs"] > r["value"]        # the reference moves ~5x the model's bytes
+    assert "reference MGS2" in r["executed_bytes_model"] and "executes" in r["unit"]
     assert sorted(r["step_seconds"]) == [1, 4, 8, 16]
     assert sum(r["step_seconds"].values()) < r["seconds_per_factorisation_sample"]
     fc = r["fit_check"]
@@ -76,7 +77,7 @@ def test_bench_cpu_baseline_measures_one_factorisation():
     assert abs(r["seconds_per_factorisation_N1e8"] / r["seconds_per_factorisation_sample"]
                - bench.N_HEADLINE / lay_N) < 0.05 * bench.N_HEADLINE / lay_N
     o = bench.cpu_baseline(16, 16, 2, variant="cgs2")
-    assert o["value"] > 0 and o["value_reference_executed_gbs"] is None
+    assert o["value"] > 0 and "4-pass CGS2" in o["executed_bytes_model"]
 
 
 def test_host_threads_respects_cpu_share(monkeypatch):

@@ -12,6 +12,55 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _gbs_fields(d, path=""):
+    """Every (path, value) of a GB/s-valued field: keys naming gbs / gbps, the top-level value and
+    roofline.achieved (unit GB/s)."""
+    if isinstance(d, dict):
+        for k, v in d.items():
+            p = f"{path}.{k}"
+            if isinstance(v, (dict, list)):
+                yield from _gbs_fields(v, p)
+            elif ("gbs" in k or "gbps" in k) and (v is None or isinstance(v, (int, float))):
+                yield p, v
+        if d.get("unit") == "GB/s":
+            for k in ("value", "achieved"):
+                if isinstance(d.get(k), (int, float)):
+                    yield f"{path}.{k}", d[k]
+    elif isinstance(d, list):
+        for i, v in enumerate(d):
+            yield from _gbs_fields(v, f"{path}[{i}]")
+
+
+def _one_byte_model(d, check_peak=False):
+    """One byte model per line: every GB/s figure is executed bytes / measured time; SURVEY 8(d)'s
+    4-pass model appears only as the dimensionless survey_model_time_ratio.  ``check_peak``: no GB/s
+    field above roofline.peak (at BASELINE size, where no vector fits the 256 MiB Infinity Cache)."""
+    gbs = list(_gbs_fields(d))
+    assert len(gbs) >= 8, gbs
+    if check_peak:
+        for path, v in gbs:
+            assert v is None or v <= d["roofline"]["peak"], (path, v)
+    assert d["survey_model_time_ratio"] > 0 and d["gram_schmidt"]["survey_model_time_ratio"] > 0
+    for k in ("effective_gbs_survey_model", "survey_headline_gbs", "last_step_survey_gbs",
+              "gpu_effective_gbs_same_model"):
+        assert k not in json.dumps(d), k
+
+
+def test_bench_full_size_no_gbs_field_above_peak(gpu):
+    """The driver's workload (config 3, N=100,014,464, m=128), one timed step: no GB/s field of the
+    line exceeds the 8 TB/s peak, the roofline fraction is the dominant kernel's."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--no-cpu",
+                        "--no-ks"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["config"]["N"] == 100_014_464 and d["config"]["m"] == 128
+    _one_byte_model(d, check_peak=True)
+    assert d["roofline"]["infinity_cache"] is None and 0.5 < d["roofline"]["frac"] < 1.0
+    assert d["survey_model_time_ratio"] > 1.0   # faster than a 4-pass CGS2 could be at roofline
+
+
 def test_bench_json_contract(gpu):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--E", "2000", "--steps", "2", "--warmup", "1",
                         "--cpu-E", "64", "--cpu-E-1core", "8"],
@@ -33,7 +82,8 @@ def test_bench_json_contract(gpu):
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
     assert cb["cores"] == cb["host"]["threads"] and cb["seconds_per_factorisation_N1e8"] > 0
-    assert cb["value_reference_executed_gbs"] > cb["value"]
+    assert cb["time_to_solution_ratio_cpu_over_gpu"] > 1
+    _one_byte_model(d)
     assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
     assert len(d["devices"]) == 1 and d["devices"][0]["pci"] and d["distinct_devices"] is True
     assert d["devices"][0]["name"]   # the marketing name, or the ISA name where libdrm has none

@@ -164,7 +164,7 @@ def test_krylov_schur_m128_real_restart_vs_oracle(gpu, mode):
         assert np.min(np.abs(exact - v)) <= 1e-10
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-lazy"])
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
 def test_config3_reduced_vs_oracle(gpu, mode):
     """Config 3 operator family at reduced N (3-D lx1=8, E=128: N=289,792), Arnoldi m=64 and
     Krylov–Schur k_dim=32, schur_tgt=4."""
@@ -177,8 +177,7 @@ def test_config3_reduced_vs_oracle(gpu, mode):
     orc.set_threads(8)
     try:
         for k, tgt in ((64, 0), (32, 4)):
-            cfg = KrylovSchurConfig(k_dim=k, schur_tgt=tgt, mode="dcgs2" if mode == "dcgs2-lazy" else mode,
-                                    lazy_basis=mode == "dcgs2-lazy")
+            cfg = KrylovSchurConfig(k_dim=k, schur_tgt=tgt, mode=mode)
             res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)
             ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, k, tgt)
             _compare_ks(res, ref, cfg)
@@ -187,13 +186,10 @@ def test_config3_reduced_vs_oracle(gpu, mode):
         orc.set_threads(1)
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-lazy"])
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
 def test_config3_full_size_properties(gpu, mode):
     """BASELINE size N=100,014,464, m=128: Ritz values vs the exact spectrum, W-orthonormality of
-    the basis and the Arnoldi relation A Q_m = Q_{m+1} H (size-independent checks); with a lazy
-    basis the returned Q is the in-place materialisation S T of the full 103 GB basis."""
-    lazy = mode == "dcgs2-lazy"
-    mode = "dcgs2" if lazy else mode
+    the basis and the Arnoldi relation A Q_m = Q_{m+1} H (size-independent checks)."""
     lay = box3d_layout(44176)
     m = 128
     w = syn.mass_weights(lay)
@@ -203,11 +199,10 @@ def test_config3_full_size_properties(gpu, mode):
     del d
     seed = ctx.vector()
     seed.fill_hash(11)
-    cfg = KrylovSchurConfig(k_dim=m, schur_tgt=0, mode=mode, lazy_basis=lazy)
+    cfg = KrylovSchurConfig(k_dim=m, schur_tgt=0, mode=mode)
     res = krylov_schur(ctx, op, seed, cfg)
     np.testing.assert_allclose(res.vals[:8].real, exact[:8], rtol=1e-10)
     Q, H = res.Q, res.H
-    assert Q.lazy == 0
     rng = np.random.default_rng(0)
     for a, b in [(0, 0), (m, m), (0, m), (5, 77), (127, 128)] + [tuple(rng.integers(0, m + 1, 2)) for _ in range(5)]:
         g = ctx.dot(Q[int(a)], Q[int(b)], False)
@@ -435,25 +430,22 @@ def test_config5_full_size_properties(gpu):
     assert abs(re - 1.0) < 1e-12 and abs(im) < 1e-12
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "dcgs2", "dcgs2-lazy"])
+@pytest.mark.parametrize("mode", ["cgs2", "dcgs2"])
 @pytest.mark.parametrize("opname", ["diag", "rot2"])
 def test_graph_replay_is_bit_identical(gpu, opname, mode):
     """cfg.graphs=True replays captured factorisations: same kernels in the same order, so the
-    Krylov–Schur result equals the eager run bit for bit (restarts exercise several mstart graphs;
-    with a lazy basis the T bookkeeping is captured too)."""
-    lazy = mode == "dcgs2-lazy"
-    mode = "dcgs2" if lazy else mode
+    Krylov–Schur result equals the eager run bit for bit (restarts exercise several mstart graphs)."""
     lay = cylinder_layout(400)
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=40)
     if opname == "diag":
         d, _ = syn.diag_spectrum(lay)
         op = DiagOperator(ctx, d)
-        cfg = dict(k_dim=16, schur_tgt=5, mode=mode, lazy_basis=lazy)
+        cfg = dict(k_dim=16, schur_tgt=5, mode=mode)
     else:
         c, s, dr, _ = syn.rot2_operator(lay)
         op = Rot2Operator(ctx, c, s, dr)
-        cfg = dict(k_dim=24, schur_tgt=2, mode=mode, lazy_basis=lazy)
+        cfg = dict(k_dim=24, schur_tgt=2, mode=mode)
     seed = ctx.vector()
     seed.fill_hash(11)
     r1 = krylov_schur(ctx, op, seed, KrylovSchurConfig(**cfg))
@@ -636,7 +628,7 @@ def test_krylov_space_closing_early(gpu, mode):
         assert np.min(np.abs(rconv - lam)) < 1e-12
 
 
-@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "dcgs2-native", "cgs2-native", "dcgs2-lazy"])
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "dcgs2-native", "cgs2-native"])
 @pytest.mark.parametrize("rank", [3, 5])
 def test_invariant_subspace_breakdown_vs_oracle(gpu, mode, rank):
     """A rank-``rank`` operator (``rank`` nonzero diagonal entries 0.95, 0.85, ...) with k_dim=16: the
@@ -655,8 +647,7 @@ def test_invariant_subspace_breakdown_vs_oracle(gpu, mode, rank):
         d[7 * (i + 1)] = exact[i]
     ctx = NekContext(lay, weights=w, max_cols=32)
     seed, q1 = _seed(ctx, lay, L, w)
-    lazy = mode == "dcgs2-lazy"
-    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=2, mode="dcgs2" if lazy else mode, lazy_basis=lazy)
+    cfg = KrylovSchurConfig(k_dim=16, schur_tgt=2, mode=mode)
     res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)
     assert res.breakdowns and res.breakdowns[0] == 1
     ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, syn.to_reference_order(lay, d)), q1, 16, 2)

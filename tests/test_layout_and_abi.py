@@ -93,7 +93,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(_lib.EXPORTED) == syms  # the ctypes table types every declared entry point
-    assert lib.nkv_abi_version() == 1
+    assert lib.nkv_abi_version() == _lib.NKV_ABI_VERSION == 2
 
 
 def test_header_constants_match_python():
@@ -101,7 +101,7 @@ def test_header_constants_match_python():
 
     txt = open(os.path.join(ROOT, "include", "nekkrylov.h")).read()
     defs = {k: int(v, 0) for k, v in re.findall(r"#define (NKV_[A-Z0-9_]+)\s+(0x[0-9a-f]+|\d+)u?", txt)}
-    for name in ("NKV_TILE", "NKV_MAX_COLS", "NKV_ROT_MAX_K", "NKV_OK", "NKV_EINVAL", "NKV_EHIP", "NKV_ENAN", "NKV_ESHAPE", "NKV_ECALLBACK",
+    for name in ("NKV_TILE", "NKV_MAX_COLS", "NKV_ROT_MAX_OUT", "NKV_OK", "NKV_EINVAL", "NKV_EHIP", "NKV_ENAN", "NKV_ESHAPE", "NKV_ECALLBACK",
                  "NKV_TIME", "NKV_ACCUMULATE", "NKV_OVERWRITE", "NKV_NORM2", "NKV_TIME_DOT", "NKV_X_IS_LAST"):
         assert defs[name] == getattr(_lib, name), name
 

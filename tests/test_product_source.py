@@ -1,36 +1,57 @@
-"""The product kernel carries no timing-experiment code paths: the
-round-1 switches that produced wrong results or could deadlock are gone from
-nekstab_next_amd/csrc/nekkrylov.hip, and build() passes no -D that could change the product."""
+"""The product kernels carry no timing-experiment code paths:
+the round-1 switches that produced wrong results or could deadlock are gone from
+nekstab_next_amd/csrc/, the kernel generations kept only for A/B (the VALU and staged-MFMA restart
+rotations, the lazy-basis DCGS2 update) were removed in round 5, and build() passes no -D that could
+change the product."""
+import glob
 import os
 import re
+import subprocess
 
 import __graft_entry__ as ge
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
+CSRC = os.path.join(ROOT, "nekstab_next_amd", "csrc")
+INTERNAL = os.path.join(CSRC, "nkv_internal.h")
 
 REMOVED = ["NKV_DC_EXPERIMENT", "NKV_DC_SYNC", "NKV_QTILE_EXP", "NKV_D2_FIELDMAJOR", "NKV_DC_SCHED",
            "NKV_D2_SCHED", "NKV_ST_AUX", "NKV_XCD_MAP", "NKV_DC_FIELDLOOP", "NKV_FUSE_PF", "NKV_LD_ALIGN"]
+RETIRED = ["k_rotate_mfma", "k_dcgs2_lazy_update", "NKV_ROT_VALU", "NKV_ROT_SMALLR", "NKV_ROT_CHUNKED", "NKV_DL_U",
+           "dcgs2_coef_lazy", "dcgs2_update_lazy", "NKV_ROT_MAX_K"]
 
 
-def test_no_experiment_switches_in_product_kernel():
-    src = open(SRC).read()
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + [INTERNAL])
+
+
+def test_build_compiles_every_translation_unit():
+    assert sorted(ge.HIP_SRCS) == sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    for src in ge.HIP_SRCS:
+        assert '#include "nkv_internal.h"' in open(src).read(), src
+
+
+def test_no_experiment_switches_in_product_kernels():
+    internal = open(INTERNAL).read()
     # the only mention allowed is the #error guard that rejects a stray -D
-    guard = src[src.index("#if defined(NKV_DC_EXPERIMENT)"):src.index("#error")]
-    body = src.replace(guard, "")
+    guard = internal[internal.index("#if defined(NKV_DC_EXPERIMENT)"):internal.index("#error")]
     for m in REMOVED:
-        assert re.search(r"\b%s\b" % m, body) is None, m
         assert m in guard, m
-    # no spin barriers / sleeps / grid-wide atomics in the product kernel
-    for pat in ("s_sleep", "s_memrealtime", "__hip_atomic"):
-        assert pat not in src, pat
+    for path in _sources():
+        body = open(path).read().replace(guard, "")
+        for m in REMOVED + RETIRED:
+            assert re.search(r"\b%s\b" % m, body) is None, (path, m)
+        # no spin barriers / sleeps / grid-wide atomics in the product kernels
+        for pat in ("s_sleep", "s_memrealtime", "__hip_atomic"):
+            assert pat not in body, (path, pat)
+    hdr = open(os.path.join(ROOT, "include", "nekkrylov.h")).read()
+    assert "lazy" not in hdr.lower() and "NKV_ROT_MAX_K" not in hdr
 
 
 def test_build_passes_no_defines():
     assert not any(f.startswith("-D") for f in ge.HIP_FLAGS)
 
 
-# ---- tuning variants derive from the product source --------------------
+# ---- tuning variants derive from the product sources -------------------
 
 def _tune():
     import importlib.util
@@ -42,38 +63,35 @@ def _tune():
 
 
 def test_no_kernel_copy_in_tools():
-    """tools/ holds no copy of the product kernel: experiments are diffs against it."""
+    """tools/ holds no copy of the product kernels: experiments are diffs against them, and every
+    speed knob a variant sets still exists in the product sources."""
     exp = os.path.join(ROOT, "tools", "experiments")
-    for f in os.listdir(exp):
-        assert f.endswith(".patch"), f
+    if os.path.isdir(exp):
+        for f in os.listdir(exp):
+            assert f.endswith(".patch"), f
     tk = _tune()
+    text = "".join(open(p).read() for p in _sources())
     for name, v in tk.VARIANTS.items():
         assert "src" not in v, name
-
-
-def test_every_experiment_patch_applies(tmp_path):
-    tk = _tune()
-    for name, v in tk.VARIANTS.items():
-        if "patch" in v:
-            out = tk.variant_source(name, out_dir=str(tmp_path))
-            assert open(out).read() != open(SRC).read(), name
+        for knob in v:
+            if knob != "patch":
+                assert re.search(r"#ifndef %s\b" % knob, text), (name, knob)
 
 
 def test_unmodified_variant_is_the_product_kernel(tmp_path):
     """The tuning tool's unpatched variant compiles to the same device code object as the product
     build (same source bytes, same flags): an A/B "base" leg is the product's kernel.  clang names
     each HIP module by a CUID hashed from its file path; both compiles get the same explicit CUID, so
-    every other byte of the code objects is compared."""
-    import subprocess
-
+    every other byte of the code objects is compared (the Gram–Schmidt translation unit)."""
     tk = _tune()
-    src = tk.variant_source("base", out_dir=str(tmp_path))
-    assert open(src, "rb").read() == open(SRC, "rb").read()
+    srcs = tk.variant_sources("base", out_dir=str(tmp_path))
+    for a, b in zip(ge.HIP_SRCS, srcs):
+        assert open(a, "rb").read() == open(b, "rb").read()
     objs = []
-    for s, tag in ((SRC, "product"), (src, "variant")):
+    for s, tag in ((os.path.join(CSRC, "gram_schmidt.hip"), "product"),
+                   (os.path.join(os.path.dirname(srcs[0]), "gram_schmidt.hip"), "variant")):
         o = str(tmp_path / f"{tag}.co")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                        "-I" + os.path.join(ROOT, "include"), "-cuid=nekkrylov", "--offload-device-only", "-c", s, "-o", o],
-                       check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", *[f for f in ge.HIP_FLAGS if f != "-fPIC"], "-cuid=nkv_gs",
+                        "--offload-device-only", "-c", s, "-o", o], check=True)
         objs.append(open(o, "rb").read())
     assert objs[0] == objs[1]

@@ -3,11 +3,14 @@
 grid size) and time the Gram–Schmidt entry points at BASELINE size in ONE process, interleaved
 over rounds (cdna_hip_programming.md §5.4 rule 24).
 
-Every variant is derived from the product source at build time: ``-D`` values of its speed knobs,
-and optionally a code experiment as a unified diff against it (``"patch": NAME`` applies
-``tools/experiments/NAME.patch`` to a copy of ``nekstab_next_amd/csrc/nekkrylov.hip``).  No copy of
-the kernel is kept: a patch that no longer applies fails the build (and the CPU test
-tests/test_product_source.py), and the unpatched variant is the product's own source.
+Every variant is derived from the product sources at build time: ``-D`` values of its speed knobs,
+and optionally a code experiment as a unified diff against them (``"patch": NAME`` applies
+``tools/experiments/NAME.patch`` with ``patch -p1`` inside a copy of ``nekstab_next_amd/csrc/``).  No
+copy of the kernels is kept: a patch that no longer applies fails the build (and the CPU test
+tests/test_product_source.py), and the unpatched variant is the product's own sources, compiled by
+the product's own build function (``__graft_entry__.build_hip``).  The round-1..3 experiment patches
+were written against the single-file source that round 5 split into per-family translation units;
+they were retired with it (git history and their logs under profiles/ keep them).
 
   python tools/tune_kernels.py build            # here (hipcc cross-compiles)
   python tools/tune_kernels.py run [--E 44176]  # on the MI355X box
@@ -22,9 +25,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "tools", "variants")
-PRODUCT_SRC = os.path.join(ROOT, "nekstab_next_amd", "csrc", "nekkrylov.hip")
+PRODUCT_CSRC = os.path.join(ROOT, "nekstab_next_amd", "csrc")
 EXP_DIR = os.path.join(ROOT, "tools", "experiments")
-HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include")]
 
 # Speed-only knobs of the product kernel.  The round-1 experiment switches (store skipping, soft
 # grid barriers, tile-interleaved / field-major sweeps, XCD maps, buffer-store policies, register-
@@ -46,8 +48,6 @@ VARIANTS = {
     "nt_fg512": {"NKV_NT": 1, "NKV_FUSE_G": 512},
     "nt_fg2048": {"NKV_NT": 1, "NKV_FUSE_G": 2048},
     "nt_f16_g512": {"NKV_NT": 1, "NKV_FUSE_NW": 16, "NKV_FUSE_G": 512},
-    "rot_valu": {"NKV_ROT_VALU": 1},
-    "rot_r32": {"NKV_ROT_SMALLR": 32},
     "rot_staged": {"NKV_ROT_STREAM": 0},
     "rot_w8": {"NKV_ROT_WAVES": 8},
     "rot_w8_nb2": {"NKV_ROT_WAVES": 8, "NKV_ROT_NB": 2},
@@ -58,7 +58,6 @@ VARIANTS = {
     "rot_pipe_u4": {"NKV_ROT_PIPE": 1, "NKV_ROT_U": 4},
     "rot_u4": {"NKV_ROT_U": 4},
     "rot_pipe_u2": {"NKV_ROT_PIPE": 1, "NKV_ROT_U": 2},
-    "rot_nochunk": {"NKV_ROT_CHUNKED": 0},
     "rot_chunk5": {"NKV_ROT_CHUNK_FROM": 5},
     "rot_nb2": {"NKV_ROT_NB": 2},
     "upd_r1": {"NKV_UPD_ROUNDS": 1},
@@ -83,7 +82,6 @@ VARIANTS = {
     "rot_chunk_w8": {"NKV_ROT_CHUNK_W8_MAX": 8},
     "rot_nb2_w8": {"NKV_ROT_NB": 2, "NKV_ROT_WAVES": 8},
     "rot_w8u8": {"NKV_ROT_WAVES": 8, "NKV_ROT_U": 8},
-    "rot_old": {"NKV_ROT_PIPE": 0, "NKV_ROT_U": 8, "NKV_ROT_CHUNKED": 0},   # rotation kernels before r02az
     "dc_u4": {"NKV_DC_U": 4},
     "dc_p4": {"NKV_DC_PAIRS": 4},
     "dc_p4_u4": {"NKV_DC_PAIRS": 4, "NKV_DC_U": 4, "NKV_D2_U": 4},
@@ -114,23 +112,12 @@ VARIANTS = {
     "st_g768": {"NKV_STREAM_G": 768},
     "dc_g896": {"NKV_DC_G": 896},
     "dc_g1536": {"NKV_DC_G": 1536},
-    "dl_u4": {"NKV_DL_U": 4},
-    "dl_u1": {"NKV_DL_U": 1},
-    "dl_g1024": {"NKV_DC_G": 1024},
-    "dl_g512": {"NKV_DC_G": 512},
     "dc_g384": {"NKV_DC_G": 384},
     "dc_r0": {"NKV_DC_ROUNDS": 0},
     "dc_r1": {"NKV_DC_ROUNDS": 1},
     "dc_r4": {"NKV_DC_ROUNDS": 4},
-    # code experiments: unified diffs against the product source (tools/experiments/*.patch).  The
-    # round-2 experiment copy (NKVX_* switches: multi-dot / block-update row bands, conflict-free LDS
-    # rotation operands, few-column rotation at 9..16 columns) was retired in round 3; its logs stay
-    # under profiles/r02*_tune_*.
-    "fuse_fw_lds": {"patch": "fuse_fw_lds"},   # fused CGS2 pass: one wave loads f and w per tile
-    "fuse_rows2": {"patch": "fuse_rows2"},     # fused CGS2 pass: two row pairs per lane, half the barriers per byte
-    "d2_prefetch": {"patch": "d2_prefetch"},   # two-vector multi-dot: next column group loaded during the reduction
-    "dcnorm_units": {"patch": "dcnorm_units"},   # fused-norm dual update: row-tile units at every size (before r03ai)
-    "d2_prefetch_ps8": {"patch": "d2_prefetch", "NKV_SMALL_TILES": 0},
+    # code experiments: unified diffs against the product sources (tools/experiments/*.patch, none
+    # at present: the round-1..3 patches targeted the pre-split single file; logs under profiles/)
     "small_tiles0": {"NKV_SMALL_TILES": 0},
     "maxb256": {"NKV_MAXB": 256},
     "maxb512": {"NKV_MAXB": 512},
@@ -150,34 +137,24 @@ VARIANTS = {
     "d2u4": {"NKV_D2_U": 4},
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
     "d2red": {"NKV_D2_RED": 1},
-    # two-vector multi-dot split into column groups at j >= NKV_D2_CG_J (round 3): fewer pages per CU
-    "d2cs2": {"patch": "d2_colsplit"},                                  # 2 groups, 256 workgroups in all
-    "d2cs2_b512": {"patch": "d2_colsplit", "NKV_D2_CG_B": 512},          # 2 groups x 256 (same tiles per block)
-    "d2cs4_b512": {"patch": "d2_colsplit", "NKV_D2_CG": 4, "NKV_D2_CG_B": 512},
-    "d2cs4_b1024": {"patch": "d2_colsplit", "NKV_D2_CG": 4, "NKV_D2_CG_B": 1024},
-    "d2cs2_j32": {"patch": "d2_colsplit", "NKV_D2_CG_J": 32},
-    "d2cs2_b512_j32": {"patch": "d2_colsplit", "NKV_D2_CG_B": 512, "NKV_D2_CG_J": 32},
-    # ... or into sequential launches over column segments (half the basis pages open at a time)
-    "d2seq2": {"patch": "d2_seqsplit"},
-    "d2seq2_j48": {"patch": "d2_seqsplit", "NKV_D2_CG_J": 48},
-    "d2seq2_j96": {"patch": "d2_seqsplit", "NKV_D2_CG_J": 96},
-    "d2seq3": {"patch": "d2_seqsplit", "NKV_D2_CG": 3},
 }
 
 
-def variant_source(name: str, out_dir: str = VDIR) -> str:
-    """The variant's source file: the product source, with the variant's patch applied if it has
-    one (``patch`` fails loudly when the diff no longer applies)."""
-    os.makedirs(out_dir, exist_ok=True)
-    out = os.path.join(out_dir, f"src_{name}.hip")
+def variant_sources(name: str, out_dir: str = VDIR) -> list:
+    """The variant's translation units: a copy of the product's csrc/ (sources + nkv_internal.h), with
+    the variant's patch applied if it has one (``patch`` fails loudly when the diff no longer applies)."""
+    import shutil
+
+    import __graft_entry__ as ge
+
+    d = os.path.join(out_dir, f"src_{name}")
+    if os.path.isdir(d):
+        shutil.rmtree(d)
+    shutil.copytree(PRODUCT_CSRC, d)
     pname = VARIANTS[name].get("patch")
     if pname:
-        pf = os.path.join(EXP_DIR, pname + ".patch")
-        subprocess.run(["patch", "-s", "-o", out, PRODUCT_SRC, pf], check=True)
-    else:
-        with open(PRODUCT_SRC, "rb") as a, open(out, "wb") as b:
-            b.write(a.read())
-    return out
+        subprocess.run(["patch", "-s", "-p1", "-d", d, "-i", os.path.join(EXP_DIR, pname + ".patch")], check=True)
+    return [os.path.join(d, os.path.basename(src)) for src in ge.HIP_SRCS]
 
 
 def variant_defines(name: str) -> list:
@@ -185,16 +162,12 @@ def variant_defines(name: str) -> list:
 
 
 def build(names):
+    import __graft_entry__ as ge
+
     os.makedirs(VDIR, exist_ok=True)
-    procs = []
-    for n in names:
-        vsrc = variant_source(n)
-        out = os.path.join(VDIR, f"lib_{n}.so")
-        # the variant source sits in tools/variants/: the product's include directory is passed explicitly
-        cmd = ["/opt/rocm/bin/hipcc", *HIP_FLAGS, *variant_defines(n), vsrc, "-o", out]
-        procs.append(subprocess.Popen(cmd))
-    for p in procs:
-        assert p.wait() == 0
+    for n in names:   # each build compiles its translation units in parallel
+        ge.build_hip(variant_sources(n), lib=os.path.join(VDIR, f"lib_{n}.so"),
+                     obj_dir=os.path.join(VDIR, f"obj_{n}"), extra_flags=variant_defines(n))
 
 
 def run(names, E, rounds, js, only=None):
@@ -277,9 +250,6 @@ def run(names, E, rounds, js, only=None):
                                                       Q[j - 1].data_ptr(), f2.data_ptr(), f2.data_ptr(), None,
                                                       ws.data_ptr(), 0x1, st),
                            8.0 * ((j - 1) * N + 4 * N)),
-            "dcgs2_lazy": (lambda: L.nkv_dcgs2_update_lazy(Lp, Q.data_ptr(), j - 1, coefs[j].data_ptr(), f.data_ptr(),
-                                                            f2.data_ptr(), ws.data_ptr(), 0x1, st),
-                           8.0 * (j * N + 2 * N)),
             "axpy_dot": (lambda: L.nkv_axpy_dot(Lp, w.data_ptr(), f2.data_ptr(), nrm1.data_ptr(), Q[0].data_ptr(),
                                                 Q[1].data_ptr(), nrm.data_ptr(), ws.data_ptr(), 0x1, st)
                          if hasattr(L, "nkv_axpy_dot") else 0, 8.0 * (3 * N + Nw + nv)),
@@ -310,8 +280,6 @@ def run(names, E, rounds, js, only=None):
                     if only and opname not in only:
                         continue
                     if opname == "rotate_part" and not hasattr(libs[n], "nkv_rotate_cols"):
-                        continue
-                    if opname == "dcgs2_lazy" and not hasattr(libs[n], "nkv_dcgs2_update_lazy"):
                         continue
                     fn()  # warm
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
