@@ -120,6 +120,24 @@ class Comm:
         if self.world > 1:
             dist.barrier(group=self.group)
 
+    def raise_if_any(self, err: BaseException | None) -> None:
+        """Collective error agreement (a barrier when no rank failed): every rank passes its own
+        failure or None; if any rank failed, EVERY rank raises — the lowest failing rank's error
+        (its own exception object there, the same type and message elsewhere) — so no rank walks on
+        into the next collective while a peer has left (the reference's nek_end stops all ranks)."""
+        if self.world == 1:
+            if err is not None:
+                raise err
+            return
+        out = [None] * self.world
+        dist.all_gather_object(out, None if err is None else (type(err).__name__, str(err)), group=self.group)
+        for r, m in enumerate(out):
+            if m is None:
+                continue
+            if r == self.rank and err is not None:
+                raise err
+            raise _PEER_ERRORS.get(m[0], RuntimeError)(f"rank {r}: {m[1]}")
+
     def min_scalar(self, x: float, device=None) -> float:
         return -self.max_scalar(-x, device=device)
 
@@ -129,6 +147,11 @@ class Comm:
         t = torch.tensor([x], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
+
+
+# error types a peer's failure is re-raised as (anything else: RuntimeError with the peer's message)
+_PEER_ERRORS = {c.__name__: c for c in (FileNotFoundError, ValueError, OSError, EOFError, KeyError, TypeError,
+                                         PermissionError, IsADirectoryError, RuntimeError)}
 
 
 def init_from_env(backend: str | None = None, force_collectives: bool = False) -> Comm:

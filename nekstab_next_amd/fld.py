@@ -222,14 +222,21 @@ def write_fld(path: str, f: FldFile) -> None:
 @contextlib.contextmanager
 def collective_output(comm, barrier: bool = True):
     """The collective end of a per-rank ``outpost2``: the body writes this rank's files (and rank
-    0's text files); on a normal exit every rank waits at a barrier until all ranks' files are in
-    place, so a read that follows on any rank finds the whole set (Nek5000's outpost2 / load_fld
-    are collective, eigensolvers.f90:607-615, sensitivity.f90:40-60).  An exception skips the
-    barrier (the peers then fail at their next collective, bounded by ``comm``'s timeout).
+    0's text files); every rank then waits until all ranks' files are in place, so a read that
+    follows on any rank finds the whole set (Nek5000's outpost2 / load_fld are collective,
+    eigensolvers.f90:607-615, sensitivity.f90:40-60).  The wait is an error agreement
+    (``Comm.raise_if_any``): when the body raises on any rank (a full disk on rank 0's HES), every
+    rank takes part and then raises, instead of its peers waiting at a barrier it never reaches.
     ``barrier=False`` exists only for the test that shows the race without it."""
-    yield
+    err = None
+    try:
+        yield
+    except Exception as e:  # noqa: BLE001 - agreed with the peers, then re-raised on every rank
+        err = e
     if barrier and comm is not None:
-        comm.barrier()
+        comm.raise_if_any(err)
+    if err is not None:
+        raise err
 
 
 def fld_name(prefix: str, session: str, fid: int, num: int) -> str:
@@ -315,9 +322,11 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
     nfileo-file set; each one's element map is checked against the prediction, and only a set
     written with another distribution (a foreign writer) falls back to reading every header.
 
-    Raises FileNotFoundError when fid 0 or any member fid < nfileo is missing (on every rank), and
-    ValueError when the files read do not cover the shard's elements — never a partial vector.  A
-    rank without elements gets one element-less FldFile carrying the set's header (time, istep)."""
+    Raises FileNotFoundError when fid 0 or any member fid < nfileo is missing, and ValueError when
+    the files read do not cover the shard's elements — never a partial vector.  With ``comm`` every
+    failure is raised on EVERY rank (``Comm.raise_if_any`` after the reads: a truncated member or a
+    shard no file covers is often one rank's alone).  A rank without elements gets one
+    element-less FldFile carrying the set's header (time, istep)."""
     def path(fid):
         return os.path.join(directory, fld_name(prefix, session, fid, num))
 
@@ -340,36 +349,49 @@ def read_fld_set(directory: str, prefix: str, session: str, num: int, lay: NekLa
     if isinstance(hdr, BaseException):
         raise hdr
     n, nelgt = hdr.nfileo, hdr.nelgt
-    missing = [i for i in range(n) if not os.path.exists(path(i))]
-    if missing:
-        raise FileNotFoundError(f"{path(missing[0])} (set of {n} files, missing fids {missing})")
-    if lay is None:
-        return [read_fld(path(i)) for i in range(n)]
 
-    e0, e1 = lay.elem_range()
-    E = lay.nelgv
-    if nelgt != E:
-        raise ValueError(f"{path(0)}: nelgt={nelgt}, the layout has {E} elements")
+    def read_shard():
+        missing = [i for i in range(n) if not os.path.exists(path(i))]
+        if missing:
+            raise FileNotFoundError(f"{path(missing[0])} (set of {n} files, missing fids {missing})")
+        if lay is None:
+            return [read_fld(path(i)) for i in range(n)]
 
-    def holds_ours(emap):
-        g = emap.astype(np.int64) - 1
-        return bool(np.any((g >= e0) & (g < e1)))
+        e0, e1 = lay.elem_range()
+        E = lay.nelgv
+        if nelgt != E:
+            raise ValueError(f"{path(0)}: nelgt={nelgt}, the layout has {E} elements")
 
-    want = [i for i in range(n) if _block(i, n, E)[0] < e1 and _block(i, n, E)[1] > e0]
-    out = {i: read_fld(path(i)) for i in want}
-    if not all(np.array_equal(out[i].emap, np.arange(*_block(i, n, E)) + 1) for i in want):
-        # another element distribution: every header decides, then the files holding our elements
-        for i in range(n):
-            if i not in out and holds_ours(read_fld_header(path(i)).emap):
-                out[i] = read_fld(path(i))
-    files = [out[i] for i in sorted(out) if holds_ours(out[i].emap)]
-    covered = np.zeros(e1 - e0, dtype=bool)
-    for f in files:
-        g = f.emap.astype(np.int64) - 1
-        covered[g[(g >= e0) & (g < e1)] - e0] = True
-    if not covered.all():
-        raise ValueError(f"{prefix}{session}*.f{num:05d}: {int((~covered).sum())} of this rank's "
-                         f"{e1 - e0} elements are in no file of the set")
-    # a rank without elements gets the set's header (time, istep) with no elements, as load_fld
-    # sets time on every rank
-    return files or [hdr]
+        def holds_ours(emap):
+            g = emap.astype(np.int64) - 1
+            return bool(np.any((g >= e0) & (g < e1)))
+
+        want = [i for i in range(n) if _block(i, n, E)[0] < e1 and _block(i, n, E)[1] > e0]
+        out = {i: read_fld(path(i)) for i in want}
+        if not all(np.array_equal(out[i].emap, np.arange(*_block(i, n, E)) + 1) for i in want):
+            # another element distribution: every header decides, then the files holding our elements
+            for i in range(n):
+                if i not in out and holds_ours(read_fld_header(path(i)).emap):
+                    out[i] = read_fld(path(i))
+        files = [out[i] for i in sorted(out) if holds_ours(out[i].emap)]
+        covered = np.zeros(e1 - e0, dtype=bool)
+        for f in files:
+            g = f.emap.astype(np.int64) - 1
+            covered[g[(g >= e0) & (g < e1)] - e0] = True
+        if not covered.all():
+            raise ValueError(f"{prefix}{session}*.f{num:05d}: {int((~covered).sum())} of this rank's "
+                             f"{e1 - e0} elements are in no file of the set")
+        # a rank without elements gets the set's header (time, istep) with no elements, as load_fld
+        # sets time on every rank
+        return files or [hdr]
+
+    err = files = None
+    try:
+        files = read_shard()
+    except Exception as e:  # noqa: BLE001 - agreed with the peers below, then raised on every rank
+        err = e
+    if comm is not None and comm.world > 1:
+        comm.raise_if_any(err)
+    elif err is not None:
+        raise err
+    return files

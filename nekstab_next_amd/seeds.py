@@ -258,13 +258,15 @@ def symmetric_seed(ctx: NekContext, coords: dict, base: NekVector | None = None,
         amp = ctx.dot(vel, vel, time=False)
     else:
         b = np.asarray(bm1, dtype=np.float64).ravel()
-        if b.size < lay.n_v:
-            raise ValueError(f"bm1 holds {b.size} points, the shard has n_v={lay.n_v}")
+        if b.size != lay.n_v:   # as NekContext's weights: exactly this shard's points (a global bm1
+            # passed on rank r > 0 would silently weight with rank 0's points)
+            raise ValueError(f"bm1 holds {b.size} points, this rank's shard has n_v={lay.n_v}")
         wb = torch.zeros(max(lay.sv, 4096), dtype=torch.float64, device=ctx.device)
         wb[: lay.n_v] = torch.as_tensor(b[: lay.n_v])
         out = ctx.scal[1:2]
         ctx.call("nkv_dot", wb.data_ptr(), vel.ptr, vel.ptr, out.data_ptr(), ctx.ws.data_ptr(), 0, ctx.stream)
         amp = float(ctx.comm.allreduce_(out).item())
+        ctx.check_nan()   # the dot's NaN flag, as ctx.dot surfaces it (nek_vectors.f90:108-111)
     amp = 1e-6 / (0.50 * amp)
     for c in (0, 1, 2, 3):                          # opcmult(qx, qy, qz, amp); cmult(qp, amp)
         seg = seed.storage[c * sv:(c + 1) * sv]

@@ -322,3 +322,74 @@ def test_missing_files_raise_on_every_rank(tmp_path):
     mp.spawn(_missing_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
     for r in range(world):
         assert out[r] == ["hes missing", "set missing"], out[r]
+
+
+def _one_rank_fails_worker(rank, world, port, directory, out):
+    sys.path.insert(0, ROOT)
+    from nekstab_next_amd import fld
+    from nekstab_next_amd import synthetic as syn
+    from nekstab_next_amd.comm import Comm
+    from nekstab_next_amd.layout import box3d_layout
+
+    _init(rank, world, port)
+    try:
+        comm = Comm()
+        res = []
+        # (1) a 3-file set whose last member holds only the first half of its elements: rank 2's shard
+        #     (E=24 on 3 ranks: elements 16..23) is partly uncovered, ranks 0 and 1 read fine alone
+        g = box3d_layout(24)
+        if rank == 0:
+            for fid in range(world):
+                sh = g.shard(fid, world)
+                f = fld.fld_from_vector(sh, syn.hash_vector(sh, 4), time=1.0, istep=1)
+                if fid == world - 1:
+                    f.emap = f.emap[:4]
+                    for k in list(f.fields):
+                        f.fields[k] = f.fields[k][:4]
+                fld.write_fld(os.path.join(directory, fld.fld_name("cov", "x", fid, 1)), f)
+        comm.barrier()
+        try:
+            fld.read_fld_set(directory, "cov", "x", 1, lay=g.shard(rank, world), comm=comm)
+            res.append("read")
+        except ValueError as e:
+            res.append(("ValueError", "rank 2" in str(e) or rank == 2))
+        # (2) a truncated member on rank 1 only (its own fid): every rank raises
+        if rank == 0:
+            for fid in range(world):
+                sh = g.shard(fid, world)
+                fld.write_fld(os.path.join(directory, fld.fld_name("trc", "x", fid, 1)),
+                              fld.fld_from_vector(sh, syn.hash_vector(sh, 5), time=1.0, istep=1))
+            p1 = os.path.join(directory, fld.fld_name("trc", "x", 1, 1))
+            with open(p1, "r+b") as fh:
+                fh.truncate(os.path.getsize(p1) // 2)
+        comm.barrier()
+        try:
+            fld.read_fld_set(directory, "trc", "x", 1, lay=g.shard(rank, world), comm=comm)
+            res.append("read")
+        except Exception as e:  # noqa: BLE001
+            res.append(("raised", "rank 1" in str(e) or rank == 1))
+        # (3) a writer that fails on rank 0 only (HES on a full disk): every rank raises at the end of
+        #     collective_output instead of waiting at a barrier rank 0 never reaches
+        try:
+            with fld.collective_output(comm):
+                if rank == 0:
+                    raise OSError("No space left on device (HES)")
+            res.append("written")
+        except OSError as e:
+            res.append(("OSError", "No space left" in str(e)))
+        comm.barrier()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_rank_failures_raise_on_every_rank(tmp_path):
+    """a read failure that only one rank sees (its elements in no file of the set, or its
+    own member truncated) and a writer failure on rank 0 alone are raised on EVERY rank (error
+    agreement after the reads / at the end of collective_output), so no peer walks into the next
+    collective and hangs until the process-group timeout."""
+    world = 3
+    out = mp.Manager().dict()
+    mp.spawn(_one_rank_fails_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r] == [("ValueError", True), ("raised", True), ("OSError", True)], (r, out[r])

@@ -617,3 +617,74 @@ def test_config5_four_ranks_vs_oracle(gpu):
         assert abs(abs(ip) - 1.0) < 0.5   # <a, d> before the rescaling: O(1)
         assert abs(got["norm_grad"] - ng_ref) <= 1e-8 * ng_ref, (rank, got["norm_grad"], ng_ref)   # modes agree to 1e-9
 
+
+
+def _run_config3_full(world_rank_pair, out, port, E, m):
+    """Config 3 as BASELINE names it (3-D lx1=8, E=44,176: N=100,014,464, m=128), DCGS2, one m-step
+    factorisation + Ritz extraction (krylov_schur with schur_tgt=0) on this rank's element shard."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import KrylovSchurConfig
+        from nekstab_next_amd.krylov_schur import krylov_schur
+        from nekstab_next_amd.layout import box3d_layout
+        from nekstab_next_amd.operators import DiagOperator
+        from nekstab_next_amd.vector import NekContext
+
+        lay = box3d_layout(E).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=m + 1)
+        d, exact = syn.laplacian_shift_invert(lay)
+        op = DiagOperator(ctx, d)
+        del d
+        seed = ctx.vector()
+        seed.fill_hash(11)
+        r = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=m, schur_tgt=0, mode="dcgs2"))
+        out[(world, rank)] = (r.vals, r.residual, r.cnt_history, r.schur_cnt, r.H, exact[:8], lay.nelv)
+        print(f"config-3 rank {rank}/{world}: {lay.nelv} elements, {int((r.residual < 1e-6).sum())} converged",
+              flush=True)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_config3_full_size_eight_ranks_match_one_rank(gpu):
+    """SURVEY §8(e)'s cross-world gate at BASELINE size: config 3 at E=44,176
+    (N=100,014,464, m=128, DCGS2) on 8 gloo ranks sharing the GPU (5,522 elements, 12.9 GB of basis
+    per rank, 103 GB in all; the 8-way split of the driver's 8-GPU run) against one rank holding the
+    whole 103 GB basis.  Converged and top-8 Ritz values 1e-12 relative, converged counts identical,
+    H identical on every rank (replicated, all-reduced) and within 1e-12 of max|H| of the one-rank H
+    (only the partial-sum grouping differs); top 8 equal the exact spectrum to 1e-10."""
+    E, m = 44176, 128
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_config3_full, args=((0, 1), out, _free_port(), E, m))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    world = 8
+    port = _free_port()
+    procs = [ctx.Process(target=_run_config3_full, args=((r, world), out, port, E, m)) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    v1, r1, cnt1, sc1, H1, exact, _ = out[(1, 0)]
+    assert [out[(world, r)][6] for r in range(world)] == [5522] * 8
+    conv = r1 < 1e-6
+    sel = sorted(set(np.nonzero(conv)[0].tolist()) | set(range(8)))
+    np.testing.assert_allclose(v1[:8].real, exact, rtol=1e-10)
+    for rank in range(world):
+        v2, r2, cnt2, sc2, H2, _, _ = out[(world, rank)]
+        assert cnt2 == cnt1 and sc2 == sc1 == 0
+        assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) <= 1e-12
+        np.testing.assert_array_equal(H2, out[(world, 0)][4])   # identical H on every rank
+    assert np.max(np.abs(out[(world, 0)][4] - H1)) <= 1e-12 * np.max(np.abs(H1))

@@ -12,7 +12,7 @@ BARGS=${NKV_BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
 mkdir -p $O $O/pmcF $O/pmcW
 cd $R
 if [ "$2" == "--pytest" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest tests -m gpu ${NKV_PYTEST_ARGS:--x} -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; exit 1; }
   tail -3 $O/pytest_gpu.log
 fi
 cd /tmp && export TMPDIR=/tmp
