@@ -388,7 +388,7 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         if on_step is None:
             if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
                 raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
-                _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
+            _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
                           flags=_lib.NKV_MGS_ICWY)
             return
         mode = "mgs2-icwy"

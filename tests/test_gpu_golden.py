@@ -36,7 +36,7 @@ def _compare_ks(res, z, tol=1e-10):
     assert res.schur_cnt == int(z["schur_cnt"])
     assert res.mstart_history == z["mstart"].tolist()
     assert res.cnt_history == z["cnt"].tolist()
-    if "selected" in z.files:   # the kept eigenvalues of every restart equal MKL's selection
+    if "selected" in z:   # the kept eigenvalues of every restart equal MKL's selection
         assert len(res.selected_history) == z["selected"].shape[0]
         for got, want in zip(res.selected_history, z["selected"]):
             assert int(np.count_nonzero(got)) == int(np.count_nonzero(want))

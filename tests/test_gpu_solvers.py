@@ -580,8 +580,16 @@ def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
 def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     """uparam(1)==2.1 (the time slot inside k_dot) through Krylov–Schur restarts: the restart
     rotation and Q(mstart) <- Q(k+1) move the fields only, not time (eigensolvers.f90:421-432,
-    458-459), as the oracle does; restart trajectory and Ritz values match it (1e-10).  The seed
-    goes in as given (seed_mode "as_is"), normalised in the k_dot norm that includes time."""
+    458-459), as the oracle does.  The seed goes in as given (seed_mode "as_is"), normalised in the
+    k_dot norm that includes time.
+
+    This is the one case where the reference's result depends on its LAPACK ("Two
+    LAPACKs"): the unrotated time slots make the kept vectors depend on the Schur vectors
+    themselves, not only on the subspace they span, and MKL's and OpenBLAS's dgees/dtrsen return
+    Schur vectors differing in sign.  Against the oracle on the product's LAPACK (OpenBLAS) the
+    restart trajectory and the comparison-set Ritz values match to 1e-10; against the oracle on
+    MKL the trajectory is identical and the converged Ritz values agree to their residual level
+    (1e-6), while the unconverged ones differ at 1e-2."""
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=32, time_in_dot=True)
@@ -595,9 +603,23 @@ def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     cfg = KrylovSchurConfig(k_dim=16, schur_tgt=5, mode=mode, seed_mode="as_is", nonorth_mode=nonorth)
     res = krylov_schur(ctx, op, seed, cfg)
     dref = syn.to_reference_order(lay, d)
-    ref = orc.krylov_schur(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), q0, 16, 5)
+
+    def oracle(lapack):
+        prev = orc.use_lapack(lapack)
+        try:
+            return orc.krylov_schur(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7),
+                                    q0, 16, 5)
+        finally:
+            orc.use_lapack(prev)
+
     assert res.schur_cnt >= 1
-    _compare_ks(res, ref, cfg)
+    _compare_ks(res, oracle("openblas"), cfg)
+    ref = oracle("mkl")
+    assert res.schur_cnt == ref["schur_cnt"] and res.mstart_history == ref["mstart"]
+    assert res.cnt_history == ref["cnt"]
+    conv = ref["residual"] < cfg.eigen_tol
+    got = match_ritz(ref["vals"][conv], res.vals)
+    assert np.max(np.abs(got - ref["vals"][conv])) <= 1e-6
 
 
 @pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
