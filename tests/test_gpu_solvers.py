@@ -588,8 +588,8 @@ def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     themselves, not only on the subspace they span, and MKL's and OpenBLAS's dgees/dtrsen return
     Schur vectors differing in sign.  Against the oracle on the product's LAPACK (OpenBLAS) the
     restart trajectory and the comparison-set Ritz values match to 1e-10; against the oracle on
-    MKL the trajectory is identical and the converged Ritz values agree to their residual level
-    (1e-6), while the unconverged ones differ at 1e-2."""
+    MKL the trajectory is identical and the schur_tgt wanted Ritz values agree to 1e-8, while the
+    rest differ at 1e-4 to 1e-2."""
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=32, time_in_dot=True)
@@ -617,9 +617,13 @@ def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     ref = oracle("mkl")
     assert res.schur_cnt == ref["schur_cnt"] and res.mstart_history == ref["mstart"]
     assert res.cnt_history == ref["cnt"]
-    conv = ref["residual"] < cfg.eigen_tol
-    got = match_ritz(ref["vals"][conv], res.vals)
-    assert np.max(np.abs(got - ref["vals"][conv])) <= 1e-6
+    # the schur_tgt wanted values (0.99 ... 0.91) agree; a further "converged" value approximating
+    # the time slot's eigenvalue 0.7 differs at 3e-4: with the basis no longer orthonormal in the
+    # k_dot inner product, the residual estimate |beta e_k^T y| bounds nothing
+    want = np.argsort(-np.abs(ref["vals"]))[:cfg.schur_tgt]
+    assert np.all(ref["residual"][want] < cfg.eigen_tol)
+    got = match_ritz(ref["vals"][want], res.vals)
+    assert np.max(np.abs(got - ref["vals"][want])) <= 1e-8
 
 
 @pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
