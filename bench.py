@@ -156,7 +156,7 @@ def host_threads() -> dict:
 # ---- CPU baseline ------------------------------------------------------------------------------
 
 def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_full: int = N_HEADLINE,
-                 fit_js=(1, 32, 64, 128)):
+                 fit_js=(1, 32, 64, 128), progress: bool = False):
     """The reference algorithm timed on this host: ONE complete m-step Arnoldi factorisation (after
     one untimed warm-up step) — the synthetic matvec, then MGS + full re-orthogonalisation with
     per-field weighted dots (copy -> dot -> cmult -> sub2, krylov_decomposition.f90:68-96,
@@ -167,7 +167,8 @@ def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_f
     from DRAM: linear in N; ``tools/cpu_factorisation.py`` measured the scaling on the GPU box).
     ``fit_check``: the round-3 method (t(j) = a + b j fitted to the steps ``fit_js`` only, summed
     over j = 1..m) evaluated on this run's own step times, with its error against the measured
-    total.  ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2)."""
+    total.  ``variant="cgs2"``: the optimised CPU line (oracle/cpu_cgs2.c, blocked OpenMP CGS2).
+    ``progress``: a line on stderr every 8 steps (long samples: a silent process looks hung)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
 
@@ -205,6 +206,9 @@ def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_f
         step(c, w, col, f, Q[:j], j, wrk)                # update_hessenberg_matrix
         Q[j] = f                                         # k_copy(Q(mstep+1), f)
         t_step[j - 1] = time.perf_counter() - ts
+        if progress and (j % 8 == 0 or j == m):
+            print(f"cpu_baseline E={E_sample}: step {j}/{m}, {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
     sec_fact = time.perf_counter() - t0
     olib.orc_set_threads(1)
     del Q

@@ -5,6 +5,9 @@ SURVEY.md §8(d)'s CPU sample) on all allowed threads, each after one warm-up st
 measured seconds scale linearly in N (so the bench's E=2,000 sample, scaled to N=1e8, stands for
 the large sample) and the error of the round-3 single-step fit against each measured total.
 
+At E=44,176 (BASELINE's own N=100,014,464: a 103 GB host basis) the factorisation is measured at
+full size, nothing scaled.
+
 usage (GPU box host): python tools/cpu_factorisation.py OUT.json [E ...]"""
 import json
 import os
@@ -22,11 +25,11 @@ def main():
     host = bench.host_threads()
     rows = []
     for E in Es:
-        r = bench.cpu_baseline(E, 128, host["threads"])
+        r = bench.cpu_baseline(E, 128, host["threads"], progress=True)
         r["E"] = E
         rows.append(r)
         print(json.dumps({k: r[k] for k in ("E", "seconds_per_factorisation_sample", "seconds_per_factorisation_N1e8",
-                                            "value_reference_executed_gbs", "fit_check")}), flush=True)
+                                            "value", "fit_check")}), flush=True)
     ref = rows[-1]
     for r in rows:
         r["N1e8_seconds_vs_largest_sample"] = round(r["seconds_per_factorisation_N1e8"] /
