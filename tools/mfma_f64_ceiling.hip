@@ -1,5 +1,5 @@
 // mfma_f64_ceiling.hip — measurement tool (not product code): the f64 matrix-core rate one MI355X
-// sustains under load, to price the restart rotation (k_rotate_stream / k_rotate_mfma) against a
+// sustains under load, to price the restart rotation (k_rotate_stream / k_rotate_chunked) against a
 // measured ceiling beside the 78.6 TFLOP/s spec.  Every wave issues back-to-back
 // v_mfma_f64_16x16x4_f64 on ACC independent accumulators (no memory traffic in the loop); the
 // grid covers every CU with WAVES waves per workgroup.  Prints one JSON line per configuration.
