@@ -129,7 +129,7 @@ static_assert(NKV_FUSE_SMALL_J >= 0 && NKV_FUSE_SMALL_J <= 16,
 #endif
 // The round-1 timing experiments (store skipping, grid-wide soft barriers, tile-interleaved and
 // field-major sweeps, XCD tile maps, buffer-store cache policies, register-budget schedules;
-// DESIGN.md §6 "What did not help") are not part of this file.  The knobs above change speed only.
+// CHANGELOG.md, "What did not help") are not part of this file.  The knobs above change speed only.
 #if defined(NKV_DC_EXPERIMENT) || defined(NKV_DC_SYNC) || defined(NKV_QTILE_EXP) || defined(NKV_D2_FIELDMAJOR) || \
     defined(NKV_DC_SCHED) || defined(NKV_D2_SCHED) || defined(NKV_ST_AUX) || defined(NKV_XCD_MAP) ||           \
     defined(NKV_DC_FIELDLOOP) || defined(NKV_FUSE_PF) || defined(NKV_LD_ALIGN)

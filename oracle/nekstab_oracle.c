@@ -6,7 +6,7 @@
  * Parity status: the reference (Fortran compiled into Nek5000) cannot be built here without
  * stand-ins for Nek5000's SIZE/TOTAL headers and routines, so this restatement is checked against
  * closed-form known answers (tests/test_oracle_*.py) — "parity unpinned" against reference
- * outputs, see DESIGN.md §Oracle.
+ * outputs, see DESIGN.md §3.
  *
  * Layout (the reference's own, unpadded): one vector = [vx | vy | (vz) | t_1..t_s | pr | time],
  * each weighted field nv doubles, pressure np doubles, `time` the last double

@@ -97,3 +97,26 @@ def test_reference_byte_model_is_about_20jN():
     N, N_w, n_v = 100_014_464, 90_472_448, 22_618_112
     per_col = (bench.reference_step_bytes(N, N_w, n_v, 101) - bench.reference_step_bytes(N, N_w, n_v, 100)) / 8
     assert 18 * N < per_col < 21 * N
+
+
+def test_full_size_cpu_run_is_the_committed_measurement():
+    """The full-size CPU factorisation (profiles/cpu_full_size_latest.json, measured on the GPU box's
+    host at BASELINE's E=44,176) is read by bench.py only for that workload, and
+    the bounded sample's N-scaling stays within 40 % of it."""
+    import json
+
+    import bench
+
+    fj = json.load(open(os.path.join(bench.ROOT, "profiles", "cpu_full_size_latest.json")))
+    r = fj["runs"][0]
+    assert r["E"] == 44176 and fj["m"] == 128 and r["seconds_per_factorisation_N1e8"] == \
+        r["seconds_per_factorisation_sample"]
+    assert fj["tag"] and fj["head"]
+    f = bench.cpu_full_size_run(44176, 128, 2000.0)
+    assert f["seconds_per_factorisation"] == r["seconds_per_factorisation_sample"]
+    assert f["time_to_solution_ratio_cpu_over_gpu"] == round(f["seconds_per_factorisation"] / 2.0, 1)
+    assert bench.cpu_full_size_run(5522, 128, 2000.0) is None and bench.cpu_full_size_run(44176, 64, 1.0) is None
+    # the r05e bench's bounded sample (N=4.5e6, scaled x22) against the full-size measurement
+    b = json.loads(open(os.path.join(bench.ROOT, "profiles", "r05e_bench_n1.json")).read().strip().splitlines()[-1])
+    scaled = b["cpu_baseline"]["seconds_per_factorisation_N1e8"]
+    assert 0.7 < f["seconds_per_factorisation"] / scaled < 1.4

@@ -4,7 +4,7 @@ multi-dot per step plus a Q'-only re-orthogonalisation, against the column-by-co
 krylov_decomposition.f90:155-180.
 
 With Q = [q1, Q'], r^2 = <q1, q1>, g = Q'^T q1 and Q' orthonormal (it is, in the first
-factorisation: DESIGN.md §9 open directions), MGS2's coefficients follow from b = Q^T f alone:
+factorisation: DESIGN.md §10 open directions), MGS2's coefficients follow from b = Q^T f alone:
   pass 1: a1 = b1,  B1 = b' - a1 g;   pass 2: a2 = b1 - a1 r^2 - g.B1,  B2 = -a2 g
   h = (a1 + a2, B1 + B2),  f <- f - q1 h1 - Q' h'
 and the exact result is orthogonal to Q', so the rounding left by the closed form is removed by a
