@@ -120,3 +120,32 @@ def test_bench_plain_command_two_gloo_ranks_one_gpu(gpu):
     assert g["gs_ms_per_factorisation_min_over_ranks"] <= g["gs_ms_per_factorisation_max_over_ranks"]
     assert abs(d2["ritz_top8_rel_err"] - outs[1]["ritz_top8_rel_err"]) < 1e-12
     assert d2["ritz_converged"] == outs[1]["ritz_converged"]
+
+
+def test_bench_two_ranks_with_restart_and_krylov_schur_legs(gpu):
+    """The driver's multi-GPU line runs the WHOLE bench on every rank, the restart and both
+    Krylov–Schur legs included (outside the timed region).  Two gloo ranks sharing this box's GPU
+    against one rank, small E: the legs complete on both ranks and make the same discrete choices
+    (restart count, mstart and converged-count histories), with the same converged values."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["NKV_BACKEND"] = "gloo"
+    common = ["--E", "400", "--m", "48", "--steps", "1", "--warmup", "1", "--no-cpu"]
+    outs = {}
+    for n in (1, 2):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *common],
+                           capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+        assert p.returncode == 0, p.stderr[-3000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, p.stdout
+        outs[n] = json.loads(lines[0])
+    d1, d2 = outs[1], outs[2]
+    assert d2["world"] == 2
+    for leg in ("krylov_schur_leg", "krylov_schur_restart_leg"):
+        a, b = d1[leg], d2[leg]
+        assert a is not None and b is not None
+        for key in ("schur_cnt", "mstart_history", "cnt_history", "converged", "relatively_converged"):
+            assert a[key] == b[key], (leg, key, a[key], b[key])
+        assert b["top4_rel_err_vs_exact"] < 1e-10
+    assert d2["krylov_schur_restart_leg"]["schur_cnt"] >= 1
+    assert d1["restart"]["mstart"] == d2["restart"]["mstart"]
+    assert d2["restart"]["rotate_kept_ms"] > 0 and d2["restart"]["rotate_full_ms"] > 0
