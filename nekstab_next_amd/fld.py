@@ -219,18 +219,42 @@ def write_fld(path: str, f: FldFile) -> None:
         raise
 
 
+class WriteGuard:
+    """Runs the writes of a :func:`collective_output` body whose ranks must stay in lock-step
+    because the body also makes collective calls (a mode assembled with all-reduced norms, then
+    written): the first write that fails is remembered and every later write on that rank is
+    skipped, while the body — and so its collectives — carries on; ``collective_output`` then
+    raises that error on every rank.  Letting the exception escape instead would take the failing
+    rank out of the body while its peers wait in the next collective."""
+
+    def __init__(self):
+        self.error = None
+
+    def __call__(self, fn, *args, **kwargs):
+        if self.error is not None:
+            return None
+        try:
+            return fn(*args, **kwargs)
+        except Exception as e:  # noqa: BLE001 - deferred to collective_output's agreement
+            self.error = e
+            return None
+
+
 @contextlib.contextmanager
 def collective_output(comm, barrier: bool = True):
     """The collective end of a per-rank ``outpost2``: the body writes this rank's files (and rank
     0's text files); every rank then waits until all ranks' files are in place, so a read that
     follows on any rank finds the whole set (Nek5000's outpost2 / load_fld are collective,
     eigensolvers.f90:607-615, sensitivity.f90:40-60).  The wait is an error agreement
-    (``Comm.raise_if_any``): when the body raises on any rank (a full disk on rank 0's HES), every
-    rank takes part and then raises, instead of its peers waiting at a barrier it never reaches.
-    ``barrier=False`` exists only for the test that shows the race without it."""
+    (``Comm.raise_if_any``): when the body raises on any rank (a full disk on rank 0's HES), or a
+    write run through the yielded :class:`WriteGuard` failed, every rank takes part and then
+    raises, instead of its peers waiting at a barrier it never reaches.  ``barrier=False`` exists
+    only for the test that shows the race without it."""
+    guard = WriteGuard()
     err = None
     try:
-        yield
+        yield guard
+        err = guard.error
     except Exception as e:  # noqa: BLE001 - agreed with the peers, then re-raised on every rank
         err = e
     if barrier and comm is not None:

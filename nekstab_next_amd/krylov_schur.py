@@ -325,32 +325,42 @@ def outpost_ks(ctx: NekContext, res: KrylovSchurResult, outdir: str, evop: str =
 
     k = res.vecs.shape[0] if k is None else k
     lay = ctx.layout
-    os.makedirs(outdir, exist_ok=True)
-    if orthonormality:
-        G = orthonormality_report(ctx, res.Q, k)
-        if ctx.comm.rank == 0:
-            with open(os.path.join(outdir, "orthonormality.dat"), "w") as fh:
-                for i in range(k):
-                    fh.write(f"Norm of the {i + 1:4d}th mode = {np.sqrt(G[i, i]):20.14f}\n")
-                    for j in range(i + 1, k):
-                        fh.write(f"Orthogonality between mode {i + 1:4d} and mode {j + 1:4d} = {G[i, j]:15.7E}\n")
-                    fh.write("\n")
-    if ctx.comm.rank == 0:
-        with open(os.path.join(outdir, f"Spectre_H{evop}.dat"), "w") as f1, \
-                open(os.path.join(outdir, f"Spectre_NS{evop}.dat"), "w") as f2:
-            for v, r in zip(res.vals[:k], res.residual[:k]):
-                f1.write(f"{v.real:15.7E}{v.imag:15.7E}{r:15.7E}\n")
-                lt = log_transform(v)
-                f2.write(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}{r:15.7E}\n")
-    written, skipped, grad_norms = [], [], {}
-    re_v, im_v = ctx.vector(), ctx.vector()
-    conv_lines = []
+    G = orthonormality_report(ctx, res.Q, k) if orthonormality else None   # collective: before any write
     ng = None
     if coords is not None:
         from .sensitivity import NormGrad
 
         ng = NormGrad(ctx, coords)
-    with fld.collective_output(ctx.comm):   # outpost2 is collective: the set is whole on return
+
+    def text(name, lines):
+        with open(os.path.join(outdir, name), "w") as fh:
+            fh.writelines(lines)
+
+    written, skipped, grad_norms = [], [], {}
+    re_v, im_v = ctx.vector(), ctx.vector()
+    conv_lines = []
+    # outpost2 is collective: the set is whole on return.  The body's mode assembly and gradient
+    # norms are collectives too, so every file write goes through the guard: a rank whose write
+    # fails skips its later writes but keeps the ranks in lock-step, and the error is raised on
+    # every rank at the end of the block
+    with fld.collective_output(ctx.comm) as write:
+        write(os.makedirs, outdir, exist_ok=True)
+        if ctx.comm.rank == 0:
+            if G is not None:
+                lines = []
+                for i in range(k):
+                    lines.append(f"Norm of the {i + 1:4d}th mode = {np.sqrt(G[i, i]):20.14f}\n")
+                    lines += [f"Orthogonality between mode {i + 1:4d} and mode {j + 1:4d} = {G[i, j]:15.7E}\n"
+                              for j in range(i + 1, k)]
+                    lines.append("\n")
+                write(text, "orthonormality.dat", lines)
+            h_lines, ns_lines = [], []
+            for v, r in zip(res.vals[:k], res.residual[:k]):
+                h_lines.append(f"{v.real:15.7E}{v.imag:15.7E}{r:15.7E}\n")
+                lt = log_transform(v)
+                ns_lines.append(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}{r:15.7E}\n")
+            write(text, f"Spectre_H{evop}.dat", h_lines)
+            write(text, f"Spectre_NS{evop}.dat", ns_lines)
         for i in range(res.converged):
             if len(written) >= maxmodes:
                 break
@@ -367,11 +377,10 @@ def outpost_ks(ctx: NekContext, res: KrylovSchurResult, outdir: str, evop: str =
             num = len(written) + 1
             for vec, name in ((re_v, f"{evop}Re"), (im_v, f"{evop}Im")):
                 f = fld.fld_from_vector(lay, vec.to_packed(), time=float(num), istep=num)
-                fld.write_fld(os.path.join(outdir, fld.fld_name(name, session, lay.rank, num)), f)
+                write(fld.write_fld, os.path.join(outdir, fld.fld_name(name, session, lay.rank, num)), f)
             lt = log_transform(res.vals[i])
             conv_lines.append(f"{lt.real / period:15.7E}{lt.imag / period:15.7E}\n")
             written.append(i)
         if ctx.comm.rank == 0:
-            with open(os.path.join(outdir, f"Spectre_NS{evop}_conv.dat"), "w") as fh:
-                fh.writelines(conv_lines)
+            write(text, f"Spectre_NS{evop}_conv.dat", conv_lines)
     return dict(modes=written, skipped=skipped, grad_norms=grad_norms)

@@ -377,6 +377,27 @@ def _one_rank_fails_worker(rank, world, port, directory, out):
             res.append("written")
         except OSError as e:
             res.append(("OSError", "No space left" in str(e)))
+        # (4) a body that interleaves collectives with its writes (outpost_ks assembles each mode with
+        #     all-reduced norms before writing it): rank 1's first write fails; the guard skips its
+        #     later writes while the all-reduces stay in lock-step, and every rank raises at the end
+        import torch
+
+        calls = []
+
+        def wr(tag):
+            if rank == 1 and tag == 0:
+                raise OSError("disk full on rank 1")
+            calls.append(tag)
+
+        try:
+            with fld.collective_output(comm) as write:
+                for tag in range(3):
+                    t = torch.ones(1, dtype=torch.float64)
+                    dist.all_reduce(t)   # the body's collective
+                    write(wr, tag)
+            res.append("written")
+        except OSError as e:
+            res.append(("OSError", "rank 1" in str(e), list(calls)))
         comm.barrier()
         out[rank] = res
     finally:
@@ -387,9 +408,12 @@ def test_one_rank_failures_raise_on_every_rank(tmp_path):
     """a read failure that only one rank sees (its elements in no file of the set, or its
     own member truncated) and a writer failure on rank 0 alone are raised on EVERY rank (error
     agreement after the reads / at the end of collective_output), so no peer walks into the next
-    collective and hangs until the process-group timeout."""
+    collective and hangs until the process-group timeout; a write that fails inside a body which
+    also makes collective calls (outpost_ks) is deferred by the WriteGuard, so the ranks stay in
+    lock-step until that agreement."""
     world = 3
     out = mp.Manager().dict()
     mp.spawn(_one_rank_fails_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
     for r in range(world):
-        assert out[r] == [("ValueError", True), ("raised", True), ("OSError", True)], (r, out[r])
+        assert out[r][:3] == [("ValueError", True), ("raised", True), ("OSError", True)], (r, out[r])
+        assert out[r][3] == ("OSError", True, [] if r == 1 else [0, 1, 2]), (r, out[r])
