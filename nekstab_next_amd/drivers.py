@@ -50,14 +50,15 @@ def linear_stability_analysis(ctx: NekContext, A: LinearOperator, seed: NekVecto
     vecs, vals, res, info = eigs(ctx, A, X, nev=cfg.schur_tgt, tolerance=cfg.eigen_tol, transpose=transpose,
                                  schur_del=cfg.schur_del, mode=cfg.mode)
     vals_ns = np.log(vals.astype(np.complex128)) / t
-    if outdir and ctx.comm.rank == 0:
-        os.makedirs(outdir, exist_ok=True)
-        _write_spectrum(os.path.join(outdir, f"Spectrum_H{evop}.dat"), vals, res)
-        _write_spectrum(os.path.join(outdir, f"Spectrum_NS{evop}.dat"), vals_ns, res)
     if outdir:
-        os.makedirs(outdir, exist_ok=True)
         v = ctx.vector()
-        with fld.collective_output(ctx.comm):   # outpost2 is collective: the sets are whole on return
+        # outpost2 is collective: the sets are whole on return; rank 0's spectra are written inside
+        # the block too, so a failure there is raised on every rank (collective_output's agreement)
+        with fld.collective_output(ctx.comm):
+            os.makedirs(outdir, exist_ok=True)
+            if ctx.comm.rank == 0:
+                _write_spectrum(os.path.join(outdir, f"Spectrum_H{evop}.dat"), vals, res)
+                _write_spectrum(os.path.join(outdir, f"Spectrum_NS{evop}.dat"), vals_ns, res)
             for i in range(min(cfg.maxmodes, cfg.k_dim)):
                 get_vec(v, X, vecs[:, i].real, cfg.k_dim)
                 _export(ctx, v, outdir, f"{evop}Re", session, i + 1, float(i + 1))
@@ -73,15 +74,14 @@ def transient_growth_analysis(ctx: NekContext, A: LinearOperator, seed: NekVecto
     prepare_seed(seed, V[0])
     r = svds(ctx, A, U, V, nev=nev, tolerance=tolerance)
     gain = r.sigma ** 2   # energy gain, sigma = sigma**2 (linear_stab.f90:113)
-    if outdir and ctx.comm.rank == 0:
-        os.makedirs(outdir, exist_ok=True)
-        with open(os.path.join(outdir, "Spectrum_Sp.dat"), "w") as fh:
-            for s, res in zip(gain, r.residuals):
-                fh.write(f"{s:15.7E}{res:15.7E}\n")
     if outdir:
-        os.makedirs(outdir, exist_ok=True)
         v = ctx.vector()
-        with fld.collective_output(ctx.comm):
+        with fld.collective_output(ctx.comm):   # rank 0's spectrum and every rank's modes, agreed
+            os.makedirs(outdir, exist_ok=True)
+            if ctx.comm.rank == 0:
+                with open(os.path.join(outdir, "Spectrum_Sp.dat"), "w") as fh:
+                    for s, res in zip(gain, r.residuals):
+                        fh.write(f"{s:15.7E}{res:15.7E}\n")
             for i in range(min(maxmodes, nev)):
                 get_vec(v, U, r.uvecs[:, i], k_dim)
                 _export(ctx, v, outdir, "pU", session, i + 1, float(i + 1))
@@ -114,9 +114,11 @@ def resolvent_analysis(ctx: NekContext, R: LinearOperator, seed: NekVector, k_di
     prepare_seed(seed, V[0])
     r = svds(ctx, R, U, V, nev=nev, tolerance=tolerance)
     gain = r.sigma ** 2   # sigma = sigma**2 (:157)
-    if outdir and ctx.comm.rank == 0:
-        os.makedirs(outdir, exist_ok=True)
-        with open(os.path.join(outdir, f"Spectrum_S{evop}.dat"), "w") as fh:
-            for s, res in zip(gain, r.residuals):
-                fh.write(f"{s:15.7E}{res:15.7E}\n")
+    if outdir:
+        with fld.collective_output(ctx.comm):   # a failure on rank 0 is raised on every rank
+            if ctx.comm.rank == 0:
+                os.makedirs(outdir, exist_ok=True)
+                with open(os.path.join(outdir, f"Spectrum_S{evop}.dat"), "w") as fh:
+                    for s, res in zip(gain, r.residuals):
+                        fh.write(f"{s:15.7E}{res:15.7E}\n")
     return dict(sigma2=gain, residuals=r.residuals, info=r.info, U=U, V=V, svd=r)

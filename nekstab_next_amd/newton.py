@@ -85,15 +85,18 @@ def newton_krylov(ctx: NekContext, nonlinear, linearized, q: NekVector, tol: flo
             op = LegacyMatvec(mode, op)
         res.gmres.append(ts_gmres(ctx, op, f, dq, gcfg))
         k_sub2(q, dq)
-    if outdir is not None and ctx.comm.rank == 0:
-        os.makedirs(outdir, exist_ok=True)
-        with open(os.path.join(outdir, "residu_newton.dat"), "w") as fh:
-            fh.writelines(lines)
-    if outdir is not None and res.converged:
+    if outdir is not None:
         from . import fld
 
         lay = ctx.layout
-        res.path = os.path.join(outdir, fld.fld_name("BF_", session, lay.rank, 1))
+        # rank 0's residual history and every rank's base flow in one agreed block: a failure on
+        # any rank is raised on every rank
         with fld.collective_output(ctx.comm):
-            fld.write_fld(res.path, fld.fld_from_vector(lay, q.to_packed(), time=q.time, istep=res.iterations))
+            os.makedirs(outdir, exist_ok=True)
+            if ctx.comm.rank == 0:
+                with open(os.path.join(outdir, "residu_newton.dat"), "w") as fh:
+                    fh.writelines(lines)
+            if res.converged:
+                res.path = os.path.join(outdir, fld.fld_name("BF_", session, lay.rank, 1))
+                fld.write_fld(res.path, fld.fld_from_vector(lay, q.to_packed(), time=q.time, istep=res.iterations))
     return res
