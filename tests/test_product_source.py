@@ -78,6 +78,16 @@ def test_no_kernel_copy_in_tools():
                 assert re.search(r"#ifndef %s\b" % knob, text), (name, knob)
 
 
+def test_experiment_patches_apply(tmp_path):
+    """Every patch variant of the tuning tool still applies to the current product sources (an A/B
+    logged under profiles/ stays reproducible from this tree)."""
+    tk = _tune()
+    for name, v in tk.VARIANTS.items():
+        if "patch" in v:
+            srcs = tk.variant_sources(name, out_dir=str(tmp_path))
+            assert all(os.path.exists(p) for p in srcs), name
+
+
 def test_unmodified_variant_is_the_product_kernel(tmp_path):
     """The tuning tool's unpatched variant compiles to the same device code object as the product
     build (same source bytes, same flags): an A/B "base" leg is the product's kernel.  clang names

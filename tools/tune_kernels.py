@@ -137,6 +137,10 @@ VARIANTS = {
     "d2u4": {"NKV_D2_U": 4},
     "ps4_d2u4": {"NKV_PAIRS_SMALL": 4, "NKV_D2_U": 4},
     "d2red": {"NKV_D2_RED": 1},
+    # round 5: the multi-dot's next column pair loaded while the current pair is reduced (software
+    # pipeline: twice the bytes in flight per wave at one wave per SIMD); the multi-dot is the
+    # box-sensitive kernel (6.55-6.79 TB/s across boxes, the dual update 6.97-7.02)
+    "d2_pf": {"patch": "d2_prefetch"},
 }
 
 
