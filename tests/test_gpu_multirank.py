@@ -688,3 +688,102 @@ def test_config3_full_size_eight_ranks_match_one_rank(gpu):
         assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) <= 1e-12
         np.testing.assert_array_equal(H2, out[(world, 0)][4])   # identical H on every rank
     assert np.max(np.abs(out[(world, 0)][4] - H1)) <= 1e-12 * np.max(np.abs(H1))
+
+
+def _run_config5_full(world_rank_pair, out, port, E, m):
+    """Config 5 as BASELINE names it (3-D lx1=8, E=22,088: N=50,007,232, k_dim=96, two bases
+    resident) on this rank's element shard: direct and adjoint Krylov–Schur, leading modes,
+    bi-orthogonalisation; the modes are reported through W-dots with shard-independent hashed probe
+    vectors (global all-reduced scalars, identical on every rank)."""
+    rank, world = world_rank_pair
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from nekstab_next_amd import synthetic as syn
+        from nekstab_next_amd.comm import Comm
+        from nekstab_next_amd.config import KrylovSchurConfig
+        from nekstab_next_amd.krylov_schur import krylov_schur, ritz_vector
+        from nekstab_next_amd.layout import box3d_layout
+        from nekstab_next_amd.operators import DiagOperator, RankTwoPerturbed
+        from nekstab_next_amd.sensitivity import biorthogonalize
+        from nekstab_next_amd.vector import NekContext
+
+        lay = box3d_layout(E).shard(rank, world)
+        ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=m + 1)
+        d, _ = syn.diag_spectrum(lay)
+        vs = []
+        for s5 in (21, 22, 23, 24):
+            v = ctx.vector()
+            v.fill_hash(s5)
+            v.scal(1e-3)
+            vs.append(v)
+        A = RankTwoPerturbed(DiagOperator(ctx, d), *vs, sigma=50.0)
+        del d
+        seed = ctx.vector()
+        seed.fill_hash(11)
+        cfg = KrylovSchurConfig(k_dim=m, schur_tgt=2, mode="dcgs2")
+        rd = krylov_schur(ctx, A, seed, cfg)
+        ra = krylov_schur(ctx, A, seed, cfg, transpose=True)
+        dRe, dIm, aRe, aIm = (ctx.vector() for _ in range(4))
+        ritz_vector(ctx, rd.Q, rd.vecs, 0, dRe, dIm, k=m)
+        ritz_vector(ctx, ra.Q, ra.vecs, 0, aRe, aIm, k=m)
+        biorthogonalize(ctx, dRe, dIm, aRe, aIm)
+        bi = (ctx.dot(aRe, dRe, False) + ctx.dot(aIm, dIm, False), ctx.dot(aRe, dIm, False) - ctx.dot(aIm, dRe, False))
+        probes = []
+        for s5 in (31, 32):
+            p = ctx.vector()
+            p.fill_hash(s5)
+            probes.append([ctx.dot(x, p, False) for x in (dRe, dIm, aRe, aIm)])
+        out[(world, rank)] = dict(d=(rd.vals, rd.mstart_history, rd.cnt_history, rd.schur_cnt),
+                                  a=(ra.vals, ra.mstart_history, ra.cnt_history, ra.schur_cnt),
+                                  bi=bi, probes=probes, nelv=lay.nelv)
+        print(f"config-5 rank {rank}/{world}: {lay.nelv} elements, lambda_1 {rd.vals[0]:.12f}", flush=True)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_config5_full_size_four_ranks_match_one_rank(gpu):
+    """Config 5's split as BASELINE names it (4 GPUs) at its full size (E=22,088: N=50,007,232,
+    k_dim=96, two bases resident: 77.6 GB in all, 19.4 GB per rank) on 4 gloo ranks sharing the GPU
+    (5,522 elements each) against one rank: the same restart / converged-count histories, direct and
+    adjoint comparison-set Ritz values 1e-12 relative, <a, d>_W = 1 + 0i to 1e-12 on every rank, and
+    the bi-orthogonalised leading modes equal through their W-dots with two hashed probe vectors
+    (1e-10 of the largest, up to the pair's common sign)."""
+    E, m = 22088, 96
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_config5_full, args=((0, 1), out, _free_port(), E, m))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    world = 4
+    port = _free_port()
+    procs = [ctx.Process(target=_run_config5_full, args=((r, world), out, port, E, m)) for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    one = out[(1, 0)]
+    assert [out[(world, r)]["nelv"] for r in range(world)] == [5522] * 4
+    p1 = np.array(one["probes"])
+    scale = np.max(np.abs(p1))
+    for r in range(world):
+        got = out[(world, r)]
+        for key in ("d", "a"):
+            v1, mh1, ch1, sc1 = one[key]
+            v, mh, ch, sc = got[key]
+            assert (mh, ch, sc) == (mh1, ch1, sc1), (r, key)
+            sel = list(range(8))
+            np.testing.assert_allclose(np.asarray(v)[sel], np.asarray(v1)[sel], rtol=1e-12)
+        re_, im_ = got["bi"]
+        assert abs(re_ - 1.0) < 1e-12 and abs(im_) < 1e-12, (r, got["bi"])
+        pr = np.array(got["probes"])
+        sign = 1.0 if np.sum(pr * p1) >= 0 else -1.0
+        assert np.max(np.abs(sign * pr - p1)) <= 1e-10 * scale, (r, pr, p1)
