@@ -619,9 +619,10 @@ def test_config5_four_ranks_vs_oracle(gpu):
 
 
 
-def _run_config3_full(world_rank_pair, out, port, E, m):
+def _run_config3_full(world_rank_pair, out, port, E, m, spectrum="shift_invert", tgt=0):
     """Config 3 as BASELINE names it (3-D lx1=8, E=44,176: N=100,014,464, m=128), DCGS2, one m-step
-    factorisation + Ritz extraction (krylov_schur with schur_tgt=0) on this rank's element shard."""
+    factorisation + Ritz extraction (krylov_schur with schur_tgt=0) on this rank's element shard;
+    ``spectrum="clustered", tgt=4``: bench.py's restart leg (a Krylov–Schur solve with a restart)."""
     rank, world = world_rank_pair
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -640,13 +641,14 @@ def _run_config3_full(world_rank_pair, out, port, E, m):
 
         lay = box3d_layout(E).shard(rank, world)
         ctx = NekContext(lay, weights=syn.mass_weights(lay), comm=Comm(), max_cols=m + 1)
-        d, exact = syn.laplacian_shift_invert(lay)
+        d, exact = syn.laplacian_shift_invert(lay) if spectrum == "shift_invert" else syn.clustered_spectrum(lay)
         op = DiagOperator(ctx, d)
         del d
         seed = ctx.vector()
         seed.fill_hash(11)
-        r = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=m, schur_tgt=0, mode="dcgs2"))
-        out[(world, rank)] = (r.vals, r.residual, r.cnt_history, r.schur_cnt, r.H, exact[:8], lay.nelv)
+        r = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=m, schur_tgt=tgt, mode="dcgs2"))
+        out[(world, rank)] = (r.vals, r.residual, r.cnt_history, r.schur_cnt, r.H, exact[:8], lay.nelv,
+                              r.mstart_history, [np.asarray(x).tolist() for x in r.selected_history])
         print(f"config-3 rank {rank}/{world}: {lay.nelv} elements, {int((r.residual < 1e-6).sum())} converged",
               flush=True)
     finally:
@@ -677,18 +679,53 @@ def test_config3_full_size_eight_ranks_match_one_rank(gpu):
     for q in procs:
         q.join()
         assert q.exitcode == 0
-    v1, r1, cnt1, sc1, H1, exact, _ = out[(1, 0)]
+    v1, r1, cnt1, sc1, H1, exact = out[(1, 0)][:6]
     assert [out[(world, r)][6] for r in range(world)] == [5522] * 8
     conv = r1 < 1e-6
     sel = sorted(set(np.nonzero(conv)[0].tolist()) | set(range(8)))
     np.testing.assert_allclose(v1[:8].real, exact, rtol=1e-10)
     for rank in range(world):
-        v2, r2, cnt2, sc2, H2, _, _ = out[(world, rank)]
+        v2, r2, cnt2, sc2, H2 = out[(world, rank)][:5]
         assert cnt2 == cnt1 and sc2 == sc1 == 0
         assert np.max(np.abs(v2[sel] - v1[sel]) / np.abs(v1[sel])) <= 1e-12
         np.testing.assert_array_equal(H2, out[(world, 0)][4])   # identical H on every rank
     assert np.max(np.abs(out[(world, 0)][4] - H1)) <= 1e-12 * np.max(np.abs(H1))
 
+
+
+def test_config3_full_size_restart_eight_ranks_match_one_rank(gpu):
+    """The Krylov–Schur leg with a restart that the driver's 8-GPU bench line runs on every rank
+    (bench.py's krylov_schur_restart_leg: config 3's layout at E=44,176, clustered spectrum,
+    k_dim=128, schur_tgt=4; one condensation keeping 25 columns: host LAPACK replicated on the
+    all-reduced H, the kept-column rotation on each shard) on 8 gloo ranks sharing the GPU against
+    one rank: identical restart / mstart / converged-count histories and selected masks on every
+    rank, comparison-set Ritz values 1e-12 relative, H identical on every rank."""
+    E, m = 44176, 128
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_run_config3_full, args=((0, 1), out, _free_port(), E, m, "clustered", 4))
+    p.start()
+    p.join()
+    assert p.exitcode == 0
+    world = 8
+    port = _free_port()
+    procs = [ctx.Process(target=_run_config3_full, args=((r, world), out, port, E, m, "clustered", 4))
+             for r in range(world)]
+    for q in procs:
+        q.start()
+    for q in procs:
+        q.join()
+        assert q.exitcode == 0
+    v1, r1, cnt1, sc1, H1, _exact, _n, mh1, sel1 = out[(1, 0)]
+    assert sc1 >= 1 and mh1
+    sel = ritz_compare_set(v1, r1, 1e-6)
+    for rank in range(world):
+        v2, r2, cnt2, sc2, H2, _e, nelv, mh2, sel2 = out[(world, rank)]
+        assert nelv == 5522
+        assert (cnt2, sc2, mh2, sel2) == (cnt1, sc1, mh1, sel1), rank
+        assert np.max(np.abs(match_ritz(v1[sel], v2) - v1[sel]) / np.abs(v1[sel])) <= 1e-12
+        np.testing.assert_array_equal(H2, out[(world, 0)][4])
 
 def _run_config5_full(world_rank_pair, out, port, E, m):
     """Config 5 as BASELINE names it (3-D lx1=8, E=22,088: N=50,007,232, k_dim=96, two bases
