@@ -41,8 +41,17 @@ Two orthogonalisation modes share the rest of the path:
   (``arnoldi_factorization``): the Gram rows of the columns before ``mstart`` are rebuilt first.
   ``"mgs2-icwy-native"``: the same sequence inside the library (``nkv_arnoldi_factorization`` with
   ``NKV_MGS_ICWY``), bit-identical.
+* ``"mgs2-lagged"``: the same MGS2 coefficients for ANY basis with TWO reads of Q per step: the
+  second pass of a column is lagged into the next step's two-vector multi-dot as in DCGS2, with the
+  Gram matrix G = Q^T W Q in the algebra (``lagged_coefficients``: beta = (I+L)^-1 p finishes the
+  provisional column, the Arnoldi relation gives A q from A u, alpha = (I+L)^-1 Q^T W A q starts
+  the next one) and the DCGS2 dual-update kernel applying it.  G and H are kept on the host, so a
+  step synchronises once (one download of the 2j dots); the rows of the columns before ``mstart``
+  are rebuilt from the basis at the start of a factorisation, as for ``"mgs2-icwy"``.  Prototype
+  and the numerics against column-by-column MGS2: ``tools/proto_nonorth_dcgs2.py``.
 
-No step synchronises the host: H lives on the device until the factorisation ends.
+No step synchronises the host (except in ``"mgs2-lagged"``): H lives on the device until the
+factorisation ends.
 """
 from __future__ import annotations
 
@@ -283,6 +292,150 @@ def _icwy_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVecto
         tm.end("finish", 16.0 * lay.N)
 
 
+
+def _unit_lower_solve(G: np.ndarray, rhs: np.ndarray) -> np.ndarray:
+    """(I + L) x = rhs, L the strictly lower part of G (the MGS recurrence alpha_i = b_i -
+    sum_{k<i} G(i,k) alpha_k, in inverse compact WY form)."""
+    from scipy.linalg import solve_triangular
+
+    n = rhs.size
+    if n == 0:
+        return np.zeros(0)
+    return solve_triangular(G[:n, :n], rhs, lower=True, unit_diagonal=True, check_finite=False)
+
+
+def lagged_coefficients(G: np.ndarray, H: np.ndarray, hv: np.ndarray, c: int, first: bool) -> np.ndarray:
+    """Host algebra of one ``"mgs2-lagged"`` step at column c (0-based; the step's matvec acted on
+    Q[c]).  ``hv`` = the step's all-reduced two-vector multi-dot with x = Q[c], y = A Q[c]:
+    [Q[0:c+1]^T W x ; Q[0:c+1]^T W y].  Updates G (row/column c) and H (column c-1 finished,
+    column c provisional) in place and returns the DCGS2 dual-update coefficient vector
+    [x (c) | . (c+1) | 1/r, y, ., 1 | a (c)] (nkv_dcgs2_update: Q[c] <- (Q[c] - Q[0:c] a) / r,
+    Q[c+1] <- A Q[c] / r - Q[0:c] x - y Q[c]_new).
+
+    ``first``: Q[c] is final (the first step of a factorisation): its Gram row is hv[0:c+1] and
+    one MGS pass alpha = (I+L)^-1 Q^T W A q_c starts column c+1.  Otherwise Q[c] holds u, the
+    previous step's first-pass result, which the reference's second pass would turn into
+    f2 = u - Q[0:c] beta with beta = (I+L)^-1 p (p = Q[0:c]^T W u); q_c = f2 / r with
+    r^2 = u.u - 2 beta.p + beta^T G beta, H(0:c, c-1) += beta, H(c, c-1) = r, G's new row
+    (p - G beta) / r; and, from y = A u and the Arnoldi relation of the finished columns,
+    A q_c = (y - Q[0:c+1] H[0:c+1, 0:c] beta) / r, so the first pass of column c+1 is
+    alpha = (I+L)^-1 ([t ; (u.y - beta.t)/r] - G H beta) / r with t = Q[0:c]^T W y, and
+    u_next = y / r - Q[0:c+1] (H beta / r + alpha).  With G = I this is DCGS2's algebra."""
+    j = c + 1
+    coef = np.zeros(3 * c + 5)
+    if first:
+        G[c, :j] = G[:j, c] = hv[:j]
+        alpha = _unit_lower_solve(G, hv[j:2 * j])
+        z, a, rinv = alpha, np.zeros(c), 1.0
+    else:
+        p, pu, t, tu = hv[:c], hv[c], hv[j:j + c], hv[j + c]
+        Gc = G[:c, :c]
+        beta = _unit_lower_solve(G, p)
+        Gb = Gc @ beta
+        r2 = pu - 2.0 * (beta @ p) + beta @ Gb
+        if not (np.isfinite(r2) and r2 > 0.0):
+            raise _lib.NkvNaNError(_lib.NKV_ENAN, "mgs2-lagged", f"column {c} has no new direction (r^2 = {r2!r})")
+        r = float(np.sqrt(r2))
+        H[:c, c - 1] += beta
+        H[c, c - 1] = r
+        G[c, :c] = G[:c, c] = (p - Gb) / r
+        G[c, c] = 1.0
+        Hb = H[:j, :c] @ beta
+        bq = np.concatenate([t, [(tu - beta @ t) / r]])
+        alpha = _unit_lower_solve(G, (bq - G[:j, :j] @ Hb) / r)
+        z, a, rinv = Hb / r + alpha, beta, 1.0 / r
+    H[:j, c] = alpha
+    coef[:c] = z[:c]
+    coef[2 * c + 1] = rinv
+    coef[2 * c + 2] = z[c]
+    coef[2 * c + 4] = 1.0
+    coef[2 * c + 5:3 * c + 5] = a
+    return coef
+
+
+def _lagged_gram(ctx: NekContext, Q: Basis, mstart: int) -> np.ndarray:
+    """Host Gram matrix of ``"mgs2-lagged"`` ((max_cols+1)^2), rows and diagonal of columns
+    0..mstart-2 rebuilt from the basis as it stands (row mstart-1 comes from the first step's
+    multi-dot)."""
+    k1 = ctx.max_cols + 1
+    G = np.zeros((k1, k1))
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    for i in range(0, mstart - 1):
+        h = ctx.h1[: i + 1]
+        ctx.call("nkv_block_dot", w, Q.ptr, i + 1, Q.col_ptr(i), h.data_ptr(), ws, tf, st)
+        ctx.comm.allreduce_(h)
+        row = h.cpu().numpy()
+        G[i, : i + 1] = G[: i + 1, i] = row
+    return G
+
+
+def _lagged_step(ctx: NekContext, Q: Basis, H: np.ndarray, G: np.ndarray, j: int, f: NekVector,
+                 first: bool) -> None:
+    """Step j (1-based; c = j-1) of ``"mgs2-lagged"``: f = A Q[c]; one two-vector multi-dot over
+    Q[0:j]; the host algebra (:func:`lagged_coefficients`); one dual update finishing Q[c] and
+    writing the next provisional column Q[j]."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    lay, tm = ctx.layout, ctx.timer
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    c = j - 1
+    h = ctx.hd[: 2 * j]
+    if tm:
+        tm.begin("block_dot2")
+    ctx.call("nkv_block_dot2", w, Q.ptr, j, Q.col_ptr(c), f.ptr, h.data_ptr(), ws, tf | NKV_X_IS_LAST, st)
+    if tm:
+        tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
+    ctx.comm.allreduce_(h)
+    coef = lagged_coefficients(G, H, h.cpu().numpy(), c, first)
+    cd = ctx.coef[: coef.size]
+    cd.copy_(torch.from_numpy(coef))
+    if tm:
+        tm.begin("dcgs2_update")
+    ctx.call("nkv_dcgs2_update", w, Q.ptr, c, cd.data_ptr(), Q.col_ptr(c), f.ptr, Q.col_ptr(j), None, ws,
+             NKV_TIME | (NKV_TIME_DOT if tf else 0), st)
+    if tm:
+        tm.end("dcgs2_update", 8.0 * (c * lay.N + 4 * lay.N))
+
+
+def _lagged_close(ctx: NekContext, Q: Basis, H: np.ndarray, G: np.ndarray, m: int) -> None:
+    """Finish the provisional Q[m] (the reference's second pass and k_normalize of the last column):
+    beta = (I+L)^-1 Q[0:m]^T W u, u <- u - Q[0:m] beta, H(0:m, m-1) += beta, H(m, m-1) = ||u||_W,
+    Q[m] = u / ||u||_W."""
+    w, ws, st = ctx.w.data_ptr(), ctx.ws.data_ptr(), ctx.stream
+    tf = NKV_TIME if ctx.time_in_dot else 0
+    h, hb, nrm, bet = ctx.h1[: m + 1], ctx.h2[:m], ctx.scal[3:4], ctx.scal[4:5]
+    ctx.call("nkv_block_dot", w, Q.ptr, m + 1, Q.col_ptr(m), h.data_ptr(), ws, tf, st)
+    ctx.comm.allreduce_(h)
+    beta = _unit_lower_solve(G, h.cpu().numpy()[:m])
+    H[:m, m - 1] += beta
+    hb.copy_(torch.from_numpy(beta))
+    ctx.call("nkv_block_update", w, Q.ptr, m, hb.data_ptr(), Q.col_ptr(m), nrm.data_ptr(), ws,
+             NKV_TIME | NKV_NORM2 | (NKV_TIME_DOT if tf else 0), st)
+    ctx.comm.allreduce_(nrm)
+    ctx.call("nkv_normalize_dev", Q.col_ptr(m), nrm.data_ptr(), bet.data_ptr(), 0, st)
+    H[m, m - 1] = float(bet.item())
+    if not (np.isfinite(H[m, m - 1]) and H[m, m - 1] > 0.0):
+        raise _lib.NkvNaNError(_lib.NKV_ENAN, "mgs2-lagged",
+                               f"the last column has no new direction (||u|| = {H[m, m - 1]!r})")
+
+
+def _lagged_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: HessenbergDev, mstart: int,
+                          mend: int, f: NekVector, transpose: bool, on_step=None) -> None:
+    """``"mgs2-lagged"`` from column ``mstart`` to ``mend`` (1-based): H on the host for the whole
+    factorisation (uploaded before each hook and at the end)."""
+    G = _lagged_gram(ctx, Q, mstart)
+    H = Hd.download()
+    for mstep in range(mstart, mend + 1):
+        (op.rmatvec if transpose else op.matvec)(Q[mstep - 1], f)
+        _lagged_step(ctx, Q, H, G, mstep, f, first=(mstep == mstart))
+        if on_step is not None and mstep > mstart:   # column mstep-1 is final after step mstep
+            Hd.upload(H)
+            on_step(mstep - 1)
+    _lagged_close(ctx, Q, H, G, mend)
+    Hd.upload(H)
+    if on_step is not None:
+        on_step(mend)
+
 def _native_scratch(ctx: NekContext, m: int) -> torch.Tensor:
     """Device scratch of the one-call drivers (nkv_arnoldi_scratch_doubles), kept on the context."""
     need = int(ctx.lib.nkv_arnoldi_scratch_doubles(max(int(m), ctx.max_cols)))
@@ -383,6 +536,11 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
                 on_step(mstep - 1)
         _dcgs2_close(ctx, Q, Hd, mend)
         on_step(mend)
+        return
+    if mode == "mgs2-lagged":
+        if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+            raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+        _lagged_factorization(ctx, op, Q, Hd, mstart, mend, f, transpose, on_step)
         return
     if mode == "mgs2-icwy-native":   # the "mgs2-icwy" sequence inside the library (one ABI call)
         if on_step is None:

@@ -22,10 +22,12 @@ class KrylovSchurConfig:
     faithful_select: bool = True   # reproduce quicksort2's ordering quirk
     max_restarts: int = 1000       # the reference loops until converged; this bounds it
     graphs: bool = False           # replay each factorisation as a captured HIP graph (capturable ops only)
-    nonorth_mode: str = "mgs2-icwy"   # Gram–Schmidt where the basis is not orthonormal (noise/load seed,
+    nonorth_mode: str = "mgs2-lagged"   # Gram–Schmidt where the basis is not orthonormal (noise/load seed,
     #                                time in k_dot after a restart), which must be modified G-S as the
-    #                                reference's: "mgs2-icwy" (inverse compact WY form, 3 reads of Q
-    #                                per step) or "mgs2" (the reference's own per-column order)
+    #                                reference's: "mgs2-lagged" (MGS2's coefficients with the second
+    #                                pass lagged into the next multi-dot, 2 reads of Q per step; not with
+    #                                time in k_dot, where ICWY is used), "mgs2-icwy" (inverse compact WY
+    #                                form, 3 reads) or "mgs2" (the reference's own per-column order)
     breakdown_tol: float = 1e-8    # |H(c+1,c)| < tol * ||H(1:c+2,c)||: the Krylov space became invariant;
     #                                that factorisation is redone in the reference's MGS2 order
 

@@ -57,17 +57,22 @@ def _mgs2_of(mode: str) -> str:
     return "mgs2-native" if mode.endswith("-native") else "mgs2"
 
 
-def _nonorth_of(mode: str, cfg: KrylovSchurConfig) -> str:
+def _nonorth_of(mode: str, cfg: KrylovSchurConfig, time_in_dot: bool = False) -> str:
     """The mode for a basis that is not orthonormal (``cfg.nonorth_mode``; "mgs2" keeps a native
     mode's library-driven variant).  An explicit reference-order request (``cfg.mode`` "mgs2" /
     "mgs2-native") is kept as it is: its rounding is the reference's, which ICWY only equals in
-    exact arithmetic."""
+    exact arithmetic.  "mgs2-lagged" derives A q from the Arnoldi relation of the finished columns,
+    which the reference's restart breaks in the `time` slot (it rotates the fields only, defect 6):
+    with time in k_dot ICWY is used instead."""
     if mode in _MGS2:
         return mode
     if cfg.nonorth_mode == "mgs2":
         return _mgs2_of(mode)
-    if cfg.nonorth_mode != "mgs2-icwy":
-        raise ValueError(f"nonorth_mode={cfg.nonorth_mode!r}: 'mgs2-icwy' or 'mgs2'")
+    if cfg.nonorth_mode == "mgs2-lagged" and not mode.endswith("-native") and not time_in_dot:
+        return "mgs2-lagged"
+    if cfg.nonorth_mode not in ("mgs2-icwy", "mgs2-lagged"):
+        raise ValueError(f"nonorth_mode={cfg.nonorth_mode!r}: 'mgs2-lagged', 'mgs2-icwy' or 'mgs2'")
+    # the library-driven (native) modes have no lagged form: their non-orthonormal runs use ICWY
     return "mgs2-icwy-native" if mode.endswith("-native") else "mgs2-icwy"
 
 
@@ -200,7 +205,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
     # inverse compact WY form (the same coefficients, three reads of Q per step), or in the
     # reference's own operation order (cfg.nonorth_mode = "mgs2").  A resumed run (``start``) keeps
     # it too: its checkpointed basis descends from the same Q(1) (pass the original seed_mode).
-    mode = _nonorth_of(cfg.mode, cfg) if cfg.seed_mode in ("noise", "load", "symm") else cfg.mode
+    mode = _nonorth_of(cfg.mode, cfg, ctx.time_in_dot) if cfg.seed_mode in ("noise", "load", "symm") else cfg.mode
     if mode != cfg.mode:
         graphs = None
     snap = None   # Q(mstart) before a classical factorisation (DCGS2's restart-row correction rewrites it)
@@ -251,7 +256,7 @@ def krylov_schur(ctx: NekContext, op: LinearOperator, seed: NekVector, cfg: Kryl
             # the restart moves the fields but not `time` (eigensolvers.f90:421-432, 458-459), so
             # with time in k_dot (uparam(1)==2.1) the kept basis is no longer orthonormal: from here
             # on modified Gram–Schmidt is mirrored (CGS2/DCGS2 assume an orthonormal basis)
-            mode, graphs = _nonorth_of(mode, cfg), None
+            mode, graphs = _nonorth_of(mode, cfg, True), None
         res.mstart_history.append(mstart)
         res.selected_history.append(selected)
         Hd.upload(H)

@@ -44,7 +44,7 @@ def test_restart_from_checkpoint_matches_uninterrupted(gpu, tmp_path):
 
 def test_noise_seeded_restart_keeps_mgs(gpu, tmp_path):
     """The reference's default noise seed leaves Q(1) unnormalised, so the whole solve is modified
-    Gram–Schmidt ("mgs2-icwy"); a run resumed from its checkpoint (uparam(2) > 0, the same
+    Gram–Schmidt (by default "mgs2-lagged"); a run resumed from its checkpoint (uparam(2) > 0, the same
     seed_mode) must stay MGS too — a classical resume would change the factorisation — and
     reproduces the uninterrupted run."""
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=300)

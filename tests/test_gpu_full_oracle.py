@@ -322,13 +322,15 @@ def test_config3_full_size_restart_vs_complete_oracle(gpu):
 def test_noise_seed_full_size_restart_vs_complete_oracle(gpu):
     """The in-tree default seed at full size: Q(1) = A (s / ||s||), NOT renormalised
     (eigensolvers.f90:195-203, reference defect 5), so the basis is not orthonormal and every
-    factorisation runs modified Gram–Schmidt (the product: "mgs2-icwy", MGS2 in inverse compact WY
-    form, three reads of Q per step) — on config 3's layout (N=100,014,464) with the clustered
+    factorisation runs modified Gram–Schmidt (the product: by default "mgs2-lagged", MGS2's
+    coefficients with two reads of Q per step; ``NKV_FULL_ORACLE_NONORTH=mgs2-icwy`` selects the
+    inverse compact WY form, three reads) — on config 3's layout (N=100,014,464) with the clustered
     spectrum, k_dim=128, schur_tgt=4, so a restart rotates the non-orthonormal basis.  Against the
     oracle's complete run from the same first vector: identical restart / mstart / converged-count
     histories and selected masks, comparison-set Ritz values 1e-10 relative.  Measured
-    (profiles/r05l_full_oracle_noise_seed.json): mstart [26], converged [3, 17] on both sides,
-    identical selections, Ritz 8.7e-15; the oracle took 807 s, the device 6.34 s."""
+    (profiles/r05x_full_oracle_noise_seed_lagged.json, "mgs2-lagged"): mstart [26], converged
+    [3, 17] on both sides, identical selections, Ritz 7.3e-15, the device 3.97 s (ICWY,
+    profiles/r05l_*: the same histories, Ritz 8.7e-15, 6.34 s); the oracle took 793-807 s."""
     import ctypes
 
     from helpers import ritz_compare_set
@@ -344,6 +346,7 @@ def test_noise_seed_full_size_restart_vs_complete_oracle(gpu):
     seed = ctx.vector()
     seed.fill_hash(11)
     cfg = KrylovSchurConfig(k_dim=m, schur_tgt=tgt, seed_mode="noise")
+    cfg.nonorth_mode = os.environ.get("NKV_FULL_ORACLE_NONORTH", cfg.nonorth_mode)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = krylov_schur(ctx, DiagOperator(ctx, d), seed, cfg)

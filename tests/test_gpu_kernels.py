@@ -545,7 +545,7 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
 
 
 @pytest.mark.parametrize("time_dot", [True, False])
-@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "cgs2-native", "mgs2-native",
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "mgs2-lagged", "cgs2-native", "mgs2-native",
                                   "mgs2-icwy-native"])
 def test_arnoldi_with_time_component_vs_oracle(gpu, mode, time_dot):
     """The scalar `time` follows every update and the operator propagates it (time_scale); with
@@ -628,6 +628,49 @@ def test_mgs2_icwy_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     if scale != 1.0:
         assert np.max(np.abs(out["cgs2"][0] - Hr)) > 1e-6 * hmax
 
+
+
+@pytest.mark.parametrize("time_dot", [False, True])
+@pytest.mark.parametrize("scale", [0.05, 1.0, 7.0])
+def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
+    """"mgs2-lagged" (MGS2's coefficients for any basis, the second pass lagged into the next
+    step's multi-dot: two reads of Q per step, arnoldi.lagged_coefficients) on the reference's
+    non-orthonormal bases (Q(1) = scale x a unit vector, eigensolvers.f90:192-223) against the
+    oracle's MGS2 in the reference's operation order, 12 steps: H to 1e-12 of max|H|, columns to
+    1e-11; the factorisation split in two calls (Gram rows rebuilt, the split column finished by
+    the closing pass) agrees with the single call to 1e-12 of max|H|."""
+    lay = LAYOUTS["3d_scalar"]
+    w = syn.mass_weights(lay)
+    ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=time_dot)
+    L = olayout(lay, time_in_dot=time_dot)
+    d, _ = syn.diag_spectrum(lay)
+    op = DiagOperator(ctx, d, time_scale=0.7)
+    m = 12
+    q0 = syn.hash_vector(lay, 7)
+    q0[lay.time_offset] = 0.3
+    q0r = syn.to_reference_order(lay, q0)
+    orc.k_normalize(L, w, q0r)
+    q0r *= scale
+    q0 = syn.from_reference_order(lay, q0r)
+    Qr = np.zeros((m + 1, L.len))
+    Qr[0] = q0r
+    Hr = np.zeros((m + 1, m))
+    dref = syn.to_reference_order(lay, d)
+    orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
+    out = {}
+    for name, splits in (("one", [(1, m)]), ("split", [(1, 5), (6, m)])):
+        Q = ctx.basis(m + 1)
+        Q[0].from_packed(q0)
+        Hd = HessenbergDev(ctx, m)
+        for a, b in splits:
+            arnoldi_factorization(ctx, op, Q, Hd, a, b, mode="mgs2-lagged")
+        ctx.check_nan()
+        out[name] = (Hd.download(), np.stack([syn.to_reference_order(lay, Q[i].to_packed()) for i in range(m + 1)]))
+    H, Qg = out["one"]
+    hmax = np.max(np.abs(Hr))
+    assert np.max(np.abs(H - Hr)) <= 1e-12 * hmax, np.max(np.abs(H - Hr)) / hmax
+    np.testing.assert_allclose(Qg, Qr, rtol=0, atol=1e-11 * max(1.0, scale))
+    assert np.max(np.abs(out["split"][0] - H)) <= 1e-12 * hmax
 
 def test_mgs2_icwy_solve_entry(gpu):
     """nkv_mgs_icwy_solve alone: x = (I + L)^{-1} b for a random row-major Gram matrix (the new row

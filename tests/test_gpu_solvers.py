@@ -478,7 +478,8 @@ def test_krylov_schur_knobs(gpu):
     q1 = np.zeros(L.len)
     orc.lib().orc_op_diag(ctypes.byref(L.c), dref, sn, q1, 0.0)
     ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
-    for nonorth, mode in (("mgs2-icwy", "dcgs2"), ("mgs2", "dcgs2"), ("mgs2-icwy", "dcgs2-native")):
+    for nonorth, mode in (("mgs2-icwy", "dcgs2"), ("mgs2", "dcgs2"), ("mgs2-icwy", "dcgs2-native"),
+                          ("mgs2-lagged", "dcgs2")):
         # MGS in inverse compact WY form (default; in the library for a native mode) / reference order
         res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise",
                                                             nonorth_mode=nonorth, mode=mode))
@@ -507,7 +508,7 @@ def test_krylov_schur_knobs(gpu):
     np.testing.assert_allclose(np.sort(res.vals[res.residual < 1e-6].real)[::-1][:5], exact[:5], atol=1e-9)
 
 
-@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2"])
+@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2", "mgs2-lagged"])
 @pytest.mark.parametrize("transpose", [False, True])
 def test_krylov_schur_load_seed_vs_oracle(gpu, tmp_path, transpose, nonorth):
     """ifseed_load (eigensolvers.f90:210-223): mode 1's real part of an earlier run, dRe (direct) or
@@ -577,7 +578,7 @@ def test_gmres_restarts_vs_oracle(gpu, findiff, mode):
     assert np.sqrt(np.sum(np.tile(w, L.nwf) * diff * diff)) < 1e-10
 
 
-@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2"])
+@pytest.mark.parametrize("nonorth", ["mgs2-icwy", "mgs2", "mgs2-lagged"])
 @pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
 def test_krylov_schur_time_component_with_restarts(gpu, mode, nonorth):
     """uparam(1)==2.1 (the time slot inside k_dot) through Krylov–Schur restarts: the restart

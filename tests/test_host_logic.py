@@ -196,14 +196,19 @@ def test_residu_newton_fortran_e_format():
 
 def test_explicit_reference_order_kept_for_nonorthonormal_bases():
     """A noise/load/symm seed runs modified Gram–Schmidt; an explicit request for the reference's
-    own order (mode "mgs2" / "mgs2-native") is kept, not replaced by the ICWY form."""
+    own order (mode "mgs2" / "mgs2-native") is kept, not replaced by the lagged or ICWY form
+    (ADVICE r3)."""
     from nekstab_next_amd.config import KrylovSchurConfig
     from nekstab_next_amd.krylov_schur import _MGS2, _nonorth_of
 
     cfg = KrylovSchurConfig()
-    assert cfg.nonorth_mode == "mgs2-icwy"
+    assert cfg.nonorth_mode == "mgs2-lagged"
     assert _nonorth_of("mgs2", cfg) == "mgs2" and _nonorth_of("mgs2-native", cfg) == "mgs2-native"
-    assert _nonorth_of("dcgs2", cfg) == "mgs2-icwy" and _nonorth_of("dcgs2-native", cfg) == "mgs2-icwy-native"
+    assert _nonorth_of("dcgs2", cfg) == "mgs2-lagged" and _nonorth_of("dcgs2-native", cfg) == "mgs2-icwy-native"
+    # with time in k_dot the restart breaks the Arnoldi relation the lagged form uses: ICWY
+    assert _nonorth_of("dcgs2", cfg, time_in_dot=True) == "mgs2-icwy"
+    icwy = KrylovSchurConfig(nonorth_mode="mgs2-icwy")
+    assert _nonorth_of("dcgs2", icwy) == "mgs2-icwy" and _nonorth_of("cgs2-native", icwy) == "mgs2-icwy-native"
     assert _nonorth_of("cgs2", KrylovSchurConfig(nonorth_mode="mgs2")) in _MGS2
 
 
