@@ -202,8 +202,7 @@ for forced in (False, True):
     seed = ctx.vector()
     seed.fill_hash(11)
     for mode in ("dcgs2", "cgs2", "dcgs2-native", "cgs2-native"):
-        kw = dict(seed_mode=seed_mode, nonorth_mode=nonorth)
-        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4, mode=mode, **kw))
+        r = krylov_schur(ctx, DiagOperator(ctx, d), seed, KrylovSchurConfig(k_dim=32, schur_tgt=4, mode=mode))
         out[(forced, mode)] = (r.vals, r.H, r.mstart_history)
     assert comm.max_scalar(3.0, device=ctx.device) == 3.0
 for mode in ("dcgs2", "cgs2", "dcgs2-native", "cgs2-native"):
