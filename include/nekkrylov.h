@@ -81,6 +81,7 @@ extern "C" {
 #define NKV_MGS2 0x40u      /* update_hessenberg / arnoldi_factorization: the reference's MGS2 order */
 #define NKV_CHECK_BREAKDOWN 0x80u /* one-call factorisations: check the new H columns on return      */
 #define NKV_MGS_ICWY 0x100u /* arnoldi_factorization: both MGS passes in inverse compact WY form (3 reads) */
+#define NKV_MGS_LAGGED 0x200u /* arnoldi_factorization: MGS2 coefficients, second pass lagged (2 reads) */
 
 typedef struct nkv_layout {
     int64_t n_v;  /* live points per weighted field on this rank (lx1*ly1*lz1*nelv)  */
@@ -316,7 +317,12 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
  * compact WY form, three reads of Q per step — see nkv_mgs_icwy_solve — for the non-orthonormal bases
  * of the reference's default noise seed; the Gram rows of columns 1..mstart-2 are rebuilt first;
  * scratch: nkv_arnoldi_scratch_doubles(mend), which covers its (mend+1)^2 Gram matrix),
- * NKV_CHECK_BREAKDOWN.
+ * NKV_MGS_LAGGED (the same MGS2 coefficients with the second pass lagged into the next step's
+ * multi-dot: two reads of Q per step, nkv_lagged_coef on the host between the multi-dot and the
+ * dual update, so each step synchronises the stream once; the Gram rows of columns 0..mstart-2 are
+ * rebuilt first and H columns 0..mend-1 are downloaded, updated on the host and written back; it
+ * uses the Arnoldi relation of the columns before mstart, which the reference's restart breaks in
+ * the time slot, so not with NKV_TIME_DOT after a restart), NKV_CHECK_BREAKDOWN.
  *
  * Breakdown (both one-call factorisations).  When the operator's Krylov space closes before mend
  * (A restricted to span(Q) is invariant: a rank-deficient operator), each later f is rounding noise.
@@ -421,6 +427,22 @@ int nkv_symmetric_seed(const nkv_layout* L, const double* ym, const double* zm, 
  * system with dgels at every column for this number (:255-258); y itself still comes from dgels on
  * the final system.  k < 0 or a NULL array: returns NaN (message in nkv_last_error). */
 double nkv_givens_column(int k, double* h, double* cs, double* sn, double* g);
+
+/* ---- "mgs2-lagged" host algebra (a7 for non-orthonormal bases: the noise / load seed's unnormalised
+ * Q(1), eigensolvers.f90:192-223; update_hessenberg_matrix's two MGS passes, krylov_decomposition.f90:
+ * 155-186) -------------------------------------------------------------------------------------
+ * MGS2's coefficients alpha = (I + L)^-1 Q^T W f for ANY basis (L the strictly lower part of the Gram
+ * matrix G), with the second pass of a column lagged into the next step's two-vector multi-dot as
+ * DCGS2 does: one multi-dot and one nkv_dcgs2_update per step.  Host-only, no device work.  G:
+ * row-major (ldg >= c+1), symmetric; H: column-major (ldh >= c+1), both host memory, updated in place.
+ * stage 1 (first step of a factorisation, Q[c] final), 0 (Q[c] holds the previous step's first-pass
+ * result u; NKV_ENAN when u has no new direction), 2 (closing pass of the last column).  hv: the
+ * step's all-reduced multi-dot (stage 0/1: nkv_block_dot2 with x = Q[c], NKV_X_IS_LAST; stage 2:
+ * nkv_block_dot of Q[c] against Q[0:c+1]).  coef: 3c+5 doubles in nkv_dcgs2_update's layout
+ * (stage 2: coef[0:c] = the second pass's coefficients, for nkv_block_update).  The algebra in full:
+ * drivers.hip; nkv_arnoldi_factorization with NKV_MGS_LAGGED runs the whole sequence. */
+int nkv_lagged_coef(int c, int stage, const double* hv, double* G, int64_t ldg, double* H, int64_t ldh,
+                    double* coef);
 
 /* ---- shard-independent synthetic data ----------------------------------------------------
  * x[row] = 2*u - 1, u = hash(seed, field, global point) in [0,1) with 53 exact bits, for live

@@ -30,6 +30,7 @@ NKV_TIME_DOT = 0x10
 NKV_X_IS_LAST = 0x20
 NKV_MGS2 = 0x40
 NKV_MGS_ICWY = 0x100
+NKV_MGS_LAGGED = 0x200
 NKV_CHECK_BREAKDOWN = 0x80
 
 
@@ -115,6 +116,7 @@ _SIGNATURES = {
     "nkv_gradm1": (c_int, [_L, c_int, c_int, _P, _P, _P, _P, _P, c_int, c_int64, _P, c_int64, _P]),
     "nkv_bf_sensitivity": (c_int, [_L, _P, _P, _P, _P, _P, _P, c_int, _P]),
     "nkv_givens_column": (c_double, [c_int, _P, _P, _P, _P]),
+    "nkv_lagged_coef": (c_int, [c_int, c_int, _P, _P, c_int64, _P, c_int64, _P]),
     "nkv_gkl_coef": (c_int, [c_int, c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, c_int64, _P, _P, _P]),
 }
 

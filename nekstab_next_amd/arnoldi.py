@@ -49,6 +49,8 @@ Two orthogonalisation modes share the rest of the path:
   step synchronises once (one download of the 2j dots); the rows of the columns before ``mstart``
   are rebuilt from the basis at the start of a factorisation, as for ``"mgs2-icwy"``.  Prototype
   and the numerics against column-by-column MGS2: ``tools/proto_nonorth_dcgs2.py``.
+  ``"mgs2-lagged-native"``: the same sequence inside the library (``nkv_arnoldi_factorization`` with
+  ``NKV_MGS_LAGGED``), bit-identical (the host algebra is the library's ``nkv_lagged_coef`` in both).
 
 No step synchronises the host (except in ``"mgs2-lagged"``): H lives on the device until the
 factorisation ends.
@@ -293,63 +295,32 @@ def _icwy_step(ctx: NekContext, Q: Basis, Hd: HessenbergDev, j: int, f: NekVecto
 
 
 
-def _unit_lower_solve(G: np.ndarray, rhs: np.ndarray) -> np.ndarray:
-    """(I + L) x = rhs, L the strictly lower part of G (the MGS recurrence alpha_i = b_i -
-    sum_{k<i} G(i,k) alpha_k, in inverse compact WY form)."""
-    from scipy.linalg import solve_triangular
+def lagged_coefficients(G: np.ndarray, H: np.ndarray, hv: np.ndarray, c: int, stage: int) -> np.ndarray:
+    """Host algebra of one ``"mgs2-lagged"`` step at column c (0-based), ``nkv_lagged_coef`` of the
+    library (drivers.hip; the one-call driver runs the same function, so the two paths are
+    bit-identical).  G: the Gram matrix (row-major float64, (max_cols+1)^2), H: the Hessenberg
+    matrix (Fortran-ordered (k+1, k)), both updated in place.
 
-    n = rhs.size
-    if n == 0:
-        return np.zeros(0)
-    return solve_triangular(G[:n, :n], rhs, lower=True, unit_diagonal=True, check_finite=False)
-
-
-def lagged_coefficients(G: np.ndarray, H: np.ndarray, hv: np.ndarray, c: int, first: bool) -> np.ndarray:
-    """Host algebra of one ``"mgs2-lagged"`` step at column c (0-based; the step's matvec acted on
-    Q[c]).  ``hv`` = the step's all-reduced two-vector multi-dot with x = Q[c], y = A Q[c]:
-    [Q[0:c+1]^T W x ; Q[0:c+1]^T W y].  Updates G (row/column c) and H (column c-1 finished,
-    column c provisional) in place and returns the DCGS2 dual-update coefficient vector
-    [x (c) | . (c+1) | 1/r, y, ., 1 | a (c)] (nkv_dcgs2_update: Q[c] <- (Q[c] - Q[0:c] a) / r,
-    Q[c+1] <- A Q[c] / r - Q[0:c] x - y Q[c]_new).
-
-    ``first``: Q[c] is final (the first step of a factorisation): its Gram row is hv[0:c+1] and
-    one MGS pass alpha = (I+L)^-1 Q^T W A q_c starts column c+1.  Otherwise Q[c] holds u, the
-    previous step's first-pass result, which the reference's second pass would turn into
-    f2 = u - Q[0:c] beta with beta = (I+L)^-1 p (p = Q[0:c]^T W u); q_c = f2 / r with
+    ``stage`` 1 — the first step of a factorisation (Q[c] final): ``hv`` = [Q[0:c+1]^T W q_c ;
+    Q[0:c+1]^T W A q_c]; G's row c, then one MGS pass alpha = (I+L)^-1 Q^T W A q_c starts column
+    c+1 (L the strictly lower part of G).
+    ``stage`` 0 — Q[c] holds u, the previous step's first-pass result, which the reference's second
+    pass would turn into f2 = u - Q[0:c] beta, beta = (I+L)^-1 p (p = Q[0:c]^T W u); q_c = f2 / r with
     r^2 = u.u - 2 beta.p + beta^T G beta, H(0:c, c-1) += beta, H(c, c-1) = r, G's new row
     (p - G beta) / r; and, from y = A u and the Arnoldi relation of the finished columns,
-    A q_c = (y - Q[0:c+1] H[0:c+1, 0:c] beta) / r, so the first pass of column c+1 is
-    alpha = (I+L)^-1 ([t ; (u.y - beta.t)/r] - G H beta) / r with t = Q[0:c]^T W y, and
-    u_next = y / r - Q[0:c+1] (H beta / r + alpha).  With G = I this is DCGS2's algebra."""
-    j = c + 1
+    A q_c = (y - Q[0:c+1] H[0:c+1, 0:c] beta) / r, so column c+1's first pass is
+    alpha = (I+L)^-1 ([t ; (u.y - beta.t)/r] - G H beta) / r (t = Q[0:c]^T W y) and
+    u_next = y / r - Q[0:c+1] (H beta / r + alpha).  With G = I this is DCGS2's algebra.
+    Returns nkv_dcgs2_update's coefficient vector [x (c) | . (c+1) | 1/r, y, ., 1 | beta (c)].
+    ``stage`` 2 — the closing pass of the last column c: ``hv`` = Q[0:c]^T W u; returns beta in
+    coef[0:c] (H(0:c, c-1) += beta).  A column with no new direction raises NkvNaNError."""
+    if not (G.dtype == H.dtype == np.float64 and G.flags.c_contiguous and H.flags.f_contiguous):
+        raise ValueError("lagged_coefficients: G row-major and H column-major float64 arrays")
+    hv = np.ascontiguousarray(hv, dtype=np.float64)
     coef = np.zeros(3 * c + 5)
-    if first:
-        G[c, :j] = G[:j, c] = hv[:j]
-        alpha = _unit_lower_solve(G, hv[j:2 * j])
-        z, a, rinv = alpha, np.zeros(c), 1.0
-    else:
-        p, pu, t, tu = hv[:c], hv[c], hv[j:j + c], hv[j + c]
-        Gc = G[:c, :c]
-        beta = _unit_lower_solve(G, p)
-        Gb = Gc @ beta
-        r2 = pu - 2.0 * (beta @ p) + beta @ Gb
-        if not (np.isfinite(r2) and r2 > 0.0):
-            raise _lib.NkvNaNError(_lib.NKV_ENAN, "mgs2-lagged", f"column {c} has no new direction (r^2 = {r2!r})")
-        r = float(np.sqrt(r2))
-        H[:c, c - 1] += beta
-        H[c, c - 1] = r
-        G[c, :c] = G[:c, c] = (p - Gb) / r
-        G[c, c] = 1.0
-        Hb = H[:j, :c] @ beta
-        bq = np.concatenate([t, [(tu - beta @ t) / r]])
-        alpha = _unit_lower_solve(G, (bq - G[:j, :j] @ Hb) / r)
-        z, a, rinv = Hb / r + alpha, beta, 1.0 / r
-    H[:j, c] = alpha
-    coef[:c] = z[:c]
-    coef[2 * c + 1] = rinv
-    coef[2 * c + 2] = z[c]
-    coef[2 * c + 4] = 1.0
-    coef[2 * c + 5:3 * c + 5] = a
+    rc = _lib.load().nkv_lagged_coef(int(c), int(stage), hv.ctypes.data, G.ctypes.data, G.shape[1], H.ctypes.data,
+                                     H.shape[0], coef.ctypes.data)
+    _lib.check(rc, "nkv_lagged_coef")
     return coef
 
 
@@ -386,7 +357,7 @@ def _lagged_step(ctx: NekContext, Q: Basis, H: np.ndarray, G: np.ndarray, j: int
     if tm:
         tm.end("block_dot2", 8.0 * ((j - 1) * lay.N_w + 2 * lay.N_w + lay.n_v))
     ctx.comm.allreduce_(h)
-    coef = lagged_coefficients(G, H, h.cpu().numpy(), c, first)
+    coef = lagged_coefficients(G, H, h.cpu().numpy(), c, 1 if first else 0)
     cd = ctx.coef[: coef.size]
     cd.copy_(torch.from_numpy(coef))
     if tm:
@@ -406,8 +377,7 @@ def _lagged_close(ctx: NekContext, Q: Basis, H: np.ndarray, G: np.ndarray, m: in
     h, hb, nrm, bet = ctx.h1[: m + 1], ctx.h2[:m], ctx.scal[3:4], ctx.scal[4:5]
     ctx.call("nkv_block_dot", w, Q.ptr, m + 1, Q.col_ptr(m), h.data_ptr(), ws, tf, st)
     ctx.comm.allreduce_(h)
-    beta = _unit_lower_solve(G, h.cpu().numpy()[:m])
-    H[:m, m - 1] += beta
+    beta = lagged_coefficients(G, H, h.cpu().numpy(), m, 2)[:m]
     hb.copy_(torch.from_numpy(beta))
     ctx.call("nkv_block_update", w, Q.ptr, m, hb.data_ptr(), Q.col_ptr(m), nrm.data_ptr(), ws,
              NKV_TIME | NKV_NORM2 | (NKV_TIME_DOT if tf else 0), st)
@@ -537,6 +507,14 @@ def arnoldi_factorization(ctx: NekContext, op: LinearOperator, Q: Basis, Hd: Hes
         _dcgs2_close(ctx, Q, Hd, mend)
         on_step(mend)
         return
+    if mode == "mgs2-lagged-native":   # the "mgs2-lagged" sequence inside the library (one ABI call)
+        if on_step is None:
+            if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
+                raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")
+            _dcgs2_native(ctx, op, Q, Hd, mstart, mend, f, transpose, entry="nkv_arnoldi_factorization",
+                          flags=_lib.NKV_MGS_LAGGED)
+            return
+        mode = "mgs2-lagged"
     if mode == "mgs2-lagged":
         if mend > ctx.max_cols or mend + 1 > Hd.k + 1:
             raise ValueError(f"step {mend} exceeds max_cols {ctx.max_cols} / H size {Hd.k}")

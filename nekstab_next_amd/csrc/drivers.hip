@@ -4,6 +4,8 @@
 // the operator and the all-reduce as host callbacks.
 #include "nkv_internal.h"
 
+#include <vector>
+
 extern "C" {
 
 // ---- the whole DCGS2 factorisation, driven natively (arnoldi_factorization, krylov_decomposition.f90:
@@ -221,6 +223,102 @@ int nkv_update_hessenberg(const nkv_layout* L, const double* w, const double* Q,
     return nkv_arnoldi_finish(L, f, nrm, q_out, j, h1, h2, hcol_dev, 0, stream);
 }
 
+// ---- "mgs2-lagged" host algebra (nekstab_next_amd/arnoldi.py, lagged_coefficients): MGS2's
+// coefficients for any basis (alpha = (I + L)^-1 Q^T W f, L the strictly lower part of the Gram matrix
+// G) with the second pass of a column lagged into the next step's two-vector multi-dot, as DCGS2 does.
+// Host-only (no device work); the Python mode and the one-call driver below both run it, so the two
+// are bit-identical.  G: row-major, ldg >= c+1, symmetric (both triangles kept); H: column-major,
+// ldh >= c+1.  stage 1 (first step of a factorisation, Q[c] final): hv = [Q[0:c+1]^T W q_c ;
+// Q[0:c+1]^T W A q_c]; G row c <- hv[0:c+1], alpha = (I+L)^-1 hv[c+1:2c+2].  stage 0 (Q[c] holds u,
+// the previous first-pass result): hv = [p ; u.u ; t ; u.A u] with p = Q[0:c]^T W u, t = Q[0:c]^T W A u;
+// beta = (I+L)^-1 p, r^2 = u.u - 2 beta.p + beta^T G beta (NKV_ENAN unless > 0), H(0:c, c-1) += beta,
+// H(c, c-1) = r, G row c = (p - G beta)/r (diagonal 1), alpha = (I+L)^-1 ([t ; (u.A u - beta.t)/r] -
+// G H beta)/r with H = H(0:c+1, 0:c).  Both: H(0:c+1, c) = alpha and coef (3c+5, the layout of
+// nkv_dcgs2_update) = [x = z[0:c] | 0 (c+1) | 1/r, z[c], 0, 1 | beta], z = H beta / r + alpha (stage 1:
+// z = alpha, r = 1, beta = 0).  stage 2 (closing pass of the last column c): hv = Q[0:c]^T W u; coef[0:c]
+// = beta = (I+L)^-1 hv, H(0:c, c-1) += beta.
+static void unit_lower_solve(const double* G, int64_t ldg, int n, const double* rhs, double* x) {
+    for (int i = 0; i < n; ++i) {
+        double s = rhs[i];
+        for (int l = 0; l < i; ++l) s -= G[(int64_t)i * ldg + l] * x[l];
+        x[i] = s;
+    }
+}
+
+int nkv_lagged_coef(int c, int stage, const double* hv, double* G, int64_t ldg, double* H, int64_t ldh,
+                    double* coef) {
+    if (c < 0 || c + 1 > NKV_MAX_COLS + 1 || stage < 0 || stage > 2 || (stage != 1 && c == 0))
+        return fail(NKV_EINVAL, "lagged coefficients: c=%d, stage=%d", c, stage);
+    if (!hv || !G || !H || !coef) return fail(NKV_EINVAL, "lagged coefficients: a NULL array");
+    if (ldg < c + 1 || ldh < c + 1) return fail(NKV_EINVAL, "lagged coefficients: ldg=%lld, ldh=%lld < %d",
+                                                (long long)ldg, (long long)ldh, c + 1);
+    const int j = c + 1;
+    auto g = [G, ldg](int i, int l) -> double& { return G[(int64_t)i * ldg + l]; };
+    auto h = [H, ldh](int i, int col) -> double& { return H[(int64_t)col * ldh + i]; };
+    std::vector<double> beta(c > 0 ? c : 1), alpha(j), z(j), Gb(c > 0 ? c : 1), Hb(j), b(j);
+    if (stage == 2) {
+        unit_lower_solve(G, ldg, c, hv, beta.data());
+        for (int i = 0; i < c; ++i) {
+            h(i, c - 1) += beta[i];
+            coef[i] = beta[i];
+        }
+        return NKV_OK;
+    }
+    for (int k = 0; k < 3 * c + 5; ++k) coef[k] = 0.0;
+    double rinv = 1.0;
+    if (stage == 1) {
+        for (int i = 0; i < j; ++i) g(c, i) = g(i, c) = hv[i];
+        unit_lower_solve(G, ldg, j, hv + j, alpha.data());
+        for (int i = 0; i < j; ++i) z[i] = alpha[i];
+    } else {
+        const double* p = hv;
+        const double pu = hv[c];
+        const double* t = hv + j;
+        const double tu = hv[j + c];
+        unit_lower_solve(G, ldg, c, p, beta.data());
+        double bp = 0.0, bgb = 0.0, bt = 0.0;
+        for (int i = 0; i < c; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < c; ++l) s += g(i, l) * beta[l];
+            Gb[i] = s;
+        }
+        for (int i = 0; i < c; ++i) {
+            bp += beta[i] * p[i];
+            bgb += beta[i] * Gb[i];
+            bt += beta[i] * t[i];
+        }
+        const double r2 = pu - 2.0 * bp + bgb;
+        if (!(std::isfinite(r2) && r2 > 0.0))
+            return fail(NKV_ENAN, "mgs2-lagged: column %d has no new direction (r^2 = %.6g)", c, r2);
+        const double r = sqrt(r2);
+        for (int i = 0; i < c; ++i) h(i, c - 1) += beta[i];
+        h(c, c - 1) = r;
+        for (int i = 0; i < c; ++i) g(c, i) = g(i, c) = (p[i] - Gb[i]) / r;
+        g(c, c) = 1.0;
+        for (int i = 0; i < j; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < c; ++l) s += h(i, l) * beta[l];
+            Hb[i] = s;
+        }
+        for (int i = 0; i < j; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < j; ++l) s += g(i, l) * Hb[l];
+            const double bq = i < c ? t[i] : (tu - bt) / r;
+            b[i] = (bq - s) / r;
+        }
+        unit_lower_solve(G, ldg, j, b.data(), alpha.data());
+        for (int i = 0; i < j; ++i) z[i] = Hb[i] / r + alpha[i];
+        for (int i = 0; i < c; ++i) coef[2 * c + 5 + i] = beta[i];
+        rinv = 1.0 / r;
+    }
+    for (int i = 0; i < j; ++i) h(i, c) = alpha[i];
+    for (int i = 0; i < c; ++i) coef[i] = z[i];
+    coef[2 * c + 1] = rinv;
+    coef[2 * c + 2] = z[c];
+    coef[2 * c + 4] = 1.0;
+    return NKV_OK;
+}
+
 // arnoldi_factorization (krylov_decomposition.f90:68-96) with the per-column update above: every
 // column final when its step ends (the cgs2 / mgs2 modes of nekstab_next_amd/arnoldi.py as one call).
 int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, int mstart, int mend, double* H_dev,
@@ -234,6 +332,66 @@ int nkv_arnoldi_factorization(const nkv_layout* L, const double* w, double* Q, i
     if (mstart < 1 || mend > NKV_MAX_COLS) return fail(NKV_EINVAL, "steps %d..%d outside 1..%d", mstart, mend, NKV_MAX_COLS);
     if (mend < mstart) return NKV_OK;
     if (ldh < mend + 1) return fail(NKV_EINVAL, "ldh=%lld < mend+1=%d", (long long)ldh, mend + 1);
+    if (flags & NKV_MGS_LAGGED) {   // the "mgs2-lagged" sequence of nekstab_next_amd/arnoldi.py (_lagged_*)
+        if (flags & (NKV_MGS2 | NKV_MGS_ICWY)) return fail(NKV_EINVAL, "NKV_MGS_LAGGED excludes NKV_MGS2 / NKV_MGS_ICWY");
+        CHECK(check_ptr(w, "w"));
+        CHECK(check_ptr(ws, "ws"));
+        hipStream_t st = S(stream);
+        const unsigned tf = (flags & NKV_TIME_DOT) ? NKV_TIME : 0u;
+        const unsigned dotf = NKV_TIME | (tf ? NKV_TIME_DOT : 0u);
+        const int64_t ldg = mend + 1;
+        double* hd = scratch_dev;                  // 2(mend+1)
+        double* coef = hd + 2 * ldg;               // 3 mend + 5
+        double* nrm = coef + 3 * mend + 6;         // + 2: within nkv_arnoldi_scratch_doubles(mend)
+        double* bet = nrm + 1;
+        auto col = [L, Q](int c) { return Q + (int64_t)c * L->ld; };
+        auto reduce = [&](double* buf, int n, const char* what) -> int {
+            if (!allreduce) return NKV_OK;
+            const int rc = allreduce(ar_user, buf, n, stream);
+            return rc == 0 ? NKV_OK : fail(NKV_ECALLBACK, "allreduce callback returned %d (%s)", rc, what);
+        };
+        auto d2h = [&](double* dst, const double* src, size_t n) -> int {   // stream-ordered, then waited for
+            hipError_t e = hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            return e == hipSuccess ? NKV_OK : fail(NKV_EHIP, "mgs2-lagged: %s", hipGetErrorString(e));
+        };
+        std::vector<double> Gh((size_t)ldg * (size_t)ldg, 0.0), Hh((size_t)ldh * (size_t)mend), hv(2 * ldg),
+            ch(3 * (size_t)mend + 5);
+        CHECK(d2h(Hh.data(), H_dev, Hh.size()));
+        for (int i = 0; i + 1 < mstart; ++i) {   // Gram rows of the columns before mstart (row mstart-1: step mstart)
+            CHECK(nkv_block_dot(L, w, Q, i + 1, col(i), hd, ws, tf, stream));
+            CHECK(reduce(hd, i + 1, "Gram row"));
+            CHECK(d2h(hv.data(), hd, (size_t)(i + 1)));
+            for (int l = 0; l <= i; ++l) Gh[(size_t)i * ldg + l] = Gh[(size_t)l * ldg + i] = hv[l];
+        }
+        for (int j = mstart; j <= mend; ++j) {
+            const int c = j - 1;
+            const int rc = matvec(mv_user, col(c), f, stream);
+            if (rc != 0) return fail(NKV_ECALLBACK, "matvec callback returned %d at step %d", rc, j);
+            CHECK(nkv_block_dot2(L, w, Q, j, col(c), f, hd, ws, tf | NKV_X_IS_LAST, stream));
+            CHECK(reduce(hd, 2 * j, "multi-dot"));
+            CHECK(d2h(hv.data(), hd, (size_t)(2 * j)));
+            CHECK(nkv_lagged_coef(c, j == mstart ? 1 : 0, hv.data(), Gh.data(), ldg, Hh.data(), ldh, ch.data()));
+            NKV_HIP(hipMemcpyAsync(coef, ch.data(), (3 * (size_t)c + 5) * sizeof(double), hipMemcpyHostToDevice, st));
+            CHECK(nkv_dcgs2_update(L, w, Q, c, coef, col(c), f, col(j), nullptr, ws, dotf, stream));
+        }
+        const int m = mend;   // closing pass: finish the provisional column mend
+        CHECK(nkv_block_dot(L, w, Q, m + 1, col(m), hd, ws, tf, stream));
+        CHECK(reduce(hd, m + 1, "closing multi-dot"));
+        CHECK(d2h(hv.data(), hd, (size_t)(m + 1)));
+        CHECK(nkv_lagged_coef(m, 2, hv.data(), Gh.data(), ldg, Hh.data(), ldh, ch.data()));
+        NKV_HIP(hipMemcpyAsync(coef, ch.data(), (size_t)m * sizeof(double), hipMemcpyHostToDevice, st));
+        CHECK(nkv_block_update(L, w, Q, m, coef, col(m), nrm, ws, NKV_NORM2 | dotf, stream));
+        CHECK(reduce(nrm, 1, "norm"));
+        CHECK(nkv_normalize_dev(L, col(m), nrm, bet, 0, stream));
+        CHECK(d2h(hv.data(), bet, 1));
+        if (!(std::isfinite(hv[0]) && hv[0] > 0.0))
+            return fail(NKV_ENAN, "mgs2-lagged: the last column has no new direction (||u|| = %.6g)", hv[0]);
+        Hh[(size_t)(m - 1) * ldh + m] = hv[0];
+        NKV_HIP(hipMemcpyAsync(H_dev, Hh.data(), Hh.size() * sizeof(double), hipMemcpyHostToDevice, st));
+        NKV_HIP(hipStreamSynchronize(st));   // the host copies above must outlive the transfer
+        return (flags & NKV_CHECK_BREAKDOWN) ? check_breakdown(H_dev, ldh, mstart - 1, mend, ws, stream) : NKV_OK;
+    }
     if (flags & NKV_MGS_ICWY) {   // the "mgs2-icwy" sequence of nekstab_next_amd/arnoldi.py (_icwy_step)
         if (flags & NKV_MGS2) return fail(NKV_EINVAL, "NKV_MGS2 and NKV_MGS_ICWY are exclusive");
         CHECK(check_ptr(w, "w"));

@@ -68,11 +68,10 @@ def _nonorth_of(mode: str, cfg: KrylovSchurConfig, time_in_dot: bool = False) ->
         return mode
     if cfg.nonorth_mode == "mgs2":
         return _mgs2_of(mode)
-    if cfg.nonorth_mode == "mgs2-lagged" and not mode.endswith("-native") and not time_in_dot:
-        return "mgs2-lagged"
+    if cfg.nonorth_mode == "mgs2-lagged" and not time_in_dot:
+        return "mgs2-lagged-native" if mode.endswith("-native") else "mgs2-lagged"
     if cfg.nonorth_mode not in ("mgs2-icwy", "mgs2-lagged"):
         raise ValueError(f"nonorth_mode={cfg.nonorth_mode!r}: 'mgs2-lagged', 'mgs2-icwy' or 'mgs2'")
-    # the library-driven (native) modes have no lagged form: their non-orthonormal runs use ICWY
     return "mgs2-icwy-native" if mode.endswith("-native") else "mgs2-icwy"
 
 

@@ -546,7 +546,7 @@ def test_block_update_dot_fused_vs_numpy(gpu, j):
 
 @pytest.mark.parametrize("time_dot", [True, False])
 @pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2", "mgs2-icwy", "mgs2-lagged", "cgs2-native", "mgs2-native",
-                                  "mgs2-icwy-native"])
+                                  "mgs2-icwy-native", "mgs2-lagged-native"])
 def test_arnoldi_with_time_component_vs_oracle(gpu, mode, time_dot):
     """The scalar `time` follows every update and the operator propagates it (time_scale); with
     uparam(1)==2.1 it also enters k_dot (krylov_subspace.f90:52-54), otherwise it is carried but
@@ -638,7 +638,8 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     non-orthonormal bases (Q(1) = scale x a unit vector, eigensolvers.f90:192-223) against the
     oracle's MGS2 in the reference's operation order, 12 steps: H to 1e-12 of max|H|, columns to
     1e-11; the factorisation split in two calls (Gram rows rebuilt, the split column finished by
-    the closing pass) agrees with the single call to 1e-12 of max|H|."""
+    the closing pass) agrees with the single call to 1e-12 of max|H|; the library's one-call
+    driver (NKV_MGS_LAGGED) reproduces the Python-driven split run bit for bit."""
     lay = LAYOUTS["3d_scalar"]
     w = syn.mass_weights(lay)
     ctx = NekContext(lay, weights=w, max_cols=16, time_in_dot=time_dot)
@@ -658,12 +659,13 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     dref = syn.to_reference_order(lay, d)
     orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
     out = {}
-    for name, splits in (("one", [(1, m)]), ("split", [(1, 5), (6, m)])):
+    for name, mode, splits in (("one", "mgs2-lagged", [(1, m)]), ("split", "mgs2-lagged", [(1, 5), (6, m)]),
+                               ("native", "mgs2-lagged-native", [(1, 5), (6, m)])):
         Q = ctx.basis(m + 1)
         Q[0].from_packed(q0)
         Hd = HessenbergDev(ctx, m)
         for a, b in splits:
-            arnoldi_factorization(ctx, op, Q, Hd, a, b, mode="mgs2-lagged")
+            arnoldi_factorization(ctx, op, Q, Hd, a, b, mode=mode)
         ctx.check_nan()
         out[name] = (Hd.download(), np.stack([syn.to_reference_order(lay, Q[i].to_packed()) for i in range(m + 1)]))
     H, Qg = out["one"]
@@ -671,6 +673,9 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     assert np.max(np.abs(H - Hr)) <= 1e-12 * hmax, np.max(np.abs(H - Hr)) / hmax
     np.testing.assert_allclose(Qg, Qr, rtol=0, atol=1e-11 * max(1.0, scale))
     assert np.max(np.abs(out["split"][0] - H)) <= 1e-12 * hmax
+    # the library's one-call sequence (nkv_arnoldi_factorization, NKV_MGS_LAGGED) is the Python one
+    np.testing.assert_array_equal(out["native"][0], out["split"][0])
+    np.testing.assert_array_equal(out["native"][1], out["split"][1])
 
 def test_mgs2_icwy_solve_entry(gpu):
     """nkv_mgs_icwy_solve alone: x = (I + L)^{-1} b for a random row-major Gram matrix (the new row

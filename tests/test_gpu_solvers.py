@@ -479,7 +479,7 @@ def test_krylov_schur_knobs(gpu):
     orc.lib().orc_op_diag(ctypes.byref(L.c), dref, sn, q1, 0.0)
     ref = orc.krylov_schur(L, w, oracle_diag_matvec(L, dref), q1, 16, 5)
     for nonorth, mode in (("mgs2-icwy", "dcgs2"), ("mgs2", "dcgs2"), ("mgs2-icwy", "dcgs2-native"),
-                          ("mgs2-lagged", "dcgs2")):
+                          ("mgs2-lagged", "dcgs2"), ("mgs2-lagged", "dcgs2-native")):
         # MGS in inverse compact WY form (default; in the library for a native mode) / reference order
         res = krylov_schur(ctx, op, seed, KrylovSchurConfig(k_dim=16, schur_tgt=5, seed_mode="noise",
                                                             nonorth_mode=nonorth, mode=mode))

@@ -204,9 +204,10 @@ def test_explicit_reference_order_kept_for_nonorthonormal_bases():
     cfg = KrylovSchurConfig()
     assert cfg.nonorth_mode == "mgs2-lagged"
     assert _nonorth_of("mgs2", cfg) == "mgs2" and _nonorth_of("mgs2-native", cfg) == "mgs2-native"
-    assert _nonorth_of("dcgs2", cfg) == "mgs2-lagged" and _nonorth_of("dcgs2-native", cfg) == "mgs2-icwy-native"
+    assert _nonorth_of("dcgs2", cfg) == "mgs2-lagged" and _nonorth_of("dcgs2-native", cfg) == "mgs2-lagged-native"
     # with time in k_dot the restart breaks the Arnoldi relation the lagged form uses: ICWY
     assert _nonorth_of("dcgs2", cfg, time_in_dot=True) == "mgs2-icwy"
+    assert _nonorth_of("dcgs2-native", cfg, time_in_dot=True) == "mgs2-icwy-native"
     icwy = KrylovSchurConfig(nonorth_mode="mgs2-icwy")
     assert _nonorth_of("dcgs2", icwy) == "mgs2-icwy" and _nonorth_of("cgs2-native", icwy) == "mgs2-icwy-native"
     assert _nonorth_of("cgs2", KrylovSchurConfig(nonorth_mode="mgs2")) in _MGS2

@@ -1,4 +1,5 @@
-"""The host algebra of ``"mgs2-lagged"`` (arnoldi.lagged_coefficients) on CPU: the device kernels it
+"""The host algebra of ``"mgs2-lagged"`` (arnoldi.lagged_coefficients = the library's host-only
+nkv_lagged_coef, callable without a GPU) on CPU: the device kernels it
 drives (the two-vector multi-dot, the DCGS2 dual update, the closing block update) are emulated
 in numpy with the same coefficient layout, and the factorisation is compared with the reference's
 column-by-column MGS2 (krylov_decomposition.f90:155-186) in the W inner product — from the
@@ -7,7 +8,7 @@ restart that rotates that non-orthonormal basis (eigensolvers.f90:421-442)."""
 import numpy as np
 import scipy.linalg as sla
 
-from nekstab_next_amd.arnoldi import _unit_lower_solve, lagged_coefficients
+from nekstab_next_amd.arnoldi import lagged_coefficients
 
 
 def _problem(n=1500, seed=3):
@@ -45,15 +46,14 @@ def _lagged(A, w, Q, H, c0, c1):
         f = A @ Q[:, c]
         j = c + 1
         hv = np.concatenate([Q[:, :j].T @ (w * Q[:, c]), Q[:, :j].T @ (w * f)])
-        coef = lagged_coefficients(G, H, hv, c, first=(c == c0))
+        coef = lagged_coefficients(G, H, hv, c, 1 if c == c0 else 0)
         x, rinv, yc, sc, a = coef[:c], coef[2 * c + 1], coef[2 * c + 2], coef[2 * c + 4], coef[2 * c + 5:3 * c + 5]
         qbar = (Q[:, c] * sc - Q[:, :c] @ a) * rinv
         Q[:, c] = qbar
         Q[:, c + 1] = f * (sc * rinv) - Q[:, :c] @ x - qbar * yc
     m = c1
     p = Q[:, : m + 1].T @ (w * Q[:, m])
-    beta = _unit_lower_solve(G, p[:m])
-    H[:m, m - 1] += beta
+    beta = lagged_coefficients(G, H, p, m, 2)[:m]   # H(0:m, m-1) += beta
     u = Q[:, m] - Q[:, :m] @ beta
     H[m, m - 1] = np.sqrt(np.sum(w * u * u))
     Q[:, m] = u / H[m, m - 1]
@@ -82,8 +82,8 @@ def test_lagged_matches_mgs2_from_the_unnormalised_seed_and_after_a_restart():
     A, w, q1 = _problem()
     n, k = q1.size, 40
     assert abs(np.sqrt(np.sum(w * q1 * q1)) - 1.0) > 0.1   # the basis is far from orthonormal
-    Qr, Hr = np.zeros((n, k + 1)), np.zeros((k + 1, k))
-    Ql, Hl = np.zeros((n, k + 1)), np.zeros((k + 1, k))
+    Qr, Hr = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
+    Ql, Hl = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
     Qr[:, 0] = Ql[:, 0] = q1
     _mgs2(A, w, Qr, Hr, 0, k)
     _lagged(A, w, Ql, Hl, 0, k)
@@ -102,8 +102,8 @@ def test_lagged_with_an_orthonormal_basis_is_mgs2():
     A, w, q1 = _problem(seed=5)
     q1 = q1 / np.sqrt(np.sum(w * q1 * q1))
     n, k = q1.size, 30
-    Qr, Hr = np.zeros((n, k + 1)), np.zeros((k + 1, k))
-    Ql, Hl = np.zeros((n, k + 1)), np.zeros((k + 1, k))
+    Qr, Hr = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
+    Ql, Hl = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
     Qr[:, 0] = Ql[:, 0] = q1
     _mgs2(A, w, Qr, Hr, 0, k)
     _lagged(A, w, Ql, Hl, 0, k)
@@ -125,10 +125,24 @@ def test_lagged_flags_a_closed_krylov_space():
     A = U @ np.diag([0.9, 0.5, 0.2]) @ U.T
     w = np.ones(n)
     q1 = A @ rng.standard_normal(n)
-    Q, H = np.zeros((n, 8)), np.zeros((8, 7))
+    Q, H = np.zeros((n, 8)), np.zeros((8, 7), order="F")
     Q[:, 0] = q1
     try:
         _lagged(A, w, Q, H, 0, 7)
     except NkvNaNError:
         return
     assert 0 <= breakdown_column(H, 0, 7, 1e-8) <= 3
+
+
+def test_lagged_coef_rejects_bad_input():
+    """nkv_lagged_coef's argument checks (a status, not a crash): stage, sizes, NULL arrays."""
+    from nekstab_next_amd import _lib
+
+    lib = _lib.load()
+    a = np.zeros(64)
+    p = a.ctypes.data
+    assert lib.nkv_lagged_coef(2, 3, p, p, 3, p, 3, p) == _lib.NKV_EINVAL
+    assert lib.nkv_lagged_coef(0, 0, p, p, 1, p, 1, p) == _lib.NKV_EINVAL   # stage 0 needs a previous column
+    assert lib.nkv_lagged_coef(2, 1, p, p, 2, p, 3, p) == _lib.NKV_EINVAL   # ldg < c+1
+    assert lib.nkv_lagged_coef(2, 1, None, p, 3, p, 3, p) == _lib.NKV_EINVAL
+    assert "lagged" in _lib.last_error()
