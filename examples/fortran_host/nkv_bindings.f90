@@ -9,6 +9,7 @@ module nkv_bindings
    integer(c_int), parameter :: NKV_OK = 0, NKV_TILE = 4096
    integer(c_int), parameter :: NKV_TIME = 1, NKV_NORM2 = 8, NKV_OVERWRITE = 4, NKV_TIME_DOT = 16
    integer(c_int), parameter :: NKV_MGS_ICWY = 256
+   integer(c_int), parameter :: NKV_MGS_LAGGED = 512
    integer(c_int), parameter :: NKV_X_IS_LAST = 32, NKV_MGS2 = 64, NKV_CHECK_BREAKDOWN = 128
    integer(c_int), parameter :: NKV_ECALLBACK = 5, NKV_EBREAKDOWN = 6
 
