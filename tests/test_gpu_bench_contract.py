@@ -149,3 +149,4 @@ def test_bench_two_ranks_with_restart_and_krylov_schur_legs(gpu):
     assert d2["krylov_schur_restart_leg"]["schur_cnt"] >= 1
     assert d1["restart"]["mstart"] == d2["restart"]["mstart"]
     assert d2["restart"]["rotate_kept_ms"] > 0 and d2["restart"]["rotate_full_ms"] > 0
+    assert 0 < d2["restart"]["rotate_kept_steady_frac_hbm"] < 1
