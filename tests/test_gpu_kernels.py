@@ -637,8 +637,8 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     step's multi-dot: two reads of Q per step, arnoldi.lagged_coefficients) on the reference's
     non-orthonormal bases (Q(1) = scale x a unit vector, eigensolvers.f90:192-223) against the
     oracle's MGS2 in the reference's operation order, 12 steps: H to 1e-12 of max|H|, columns to
-    1e-11; the factorisation split in two calls (Gram rows rebuilt, the split column finished by
-    the closing pass) agrees with the single call to 1e-12 of max|H|; the library's one-call
+    1e-11; the factorisation split in two calls, or into one-column calls (Gram rows rebuilt, the
+    split column finished by the closing pass) agrees with the single call to 1e-12 of max|H|; the library's one-call
     driver (NKV_MGS_LAGGED) reproduces the Python-driven split run bit for bit."""
     lay = LAYOUTS["3d_scalar"]
     w = syn.mass_weights(lay)
@@ -660,7 +660,9 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     orc.arnoldi_factorization(L, w, lambda x, y: orc.lib().orc_op_diag(ctypes.byref(L.c), dref, x, y, 0.7), Qr, Hr, 1, m)
     out = {}
     for name, mode, splits in (("one", "mgs2-lagged", [(1, m)]), ("split", "mgs2-lagged", [(1, 5), (6, m)]),
-                               ("native", "mgs2-lagged-native", [(1, 5), (6, m)])):
+                               ("native", "mgs2-lagged-native", [(1, 5), (6, m)]),
+                               ("steps", "mgs2-lagged", [(1, 1), (2, 2), (3, 5), (6, m)]),
+                               ("native_steps", "mgs2-lagged-native", [(1, 1), (2, 2), (3, 5), (6, m)])):
         Q = ctx.basis(m + 1)
         Q[0].from_packed(q0)
         Hd = HessenbergDev(ctx, m)
@@ -676,6 +678,12 @@ def test_mgs2_lagged_nonorthonormal_basis_vs_oracle(gpu, scale, time_dot):
     # the library's one-call sequence (nkv_arnoldi_factorization, NKV_MGS_LAGGED) is the Python one
     np.testing.assert_array_equal(out["native"][0], out["split"][0])
     np.testing.assert_array_equal(out["native"][1], out["split"][1])
+    # one-column calls (mstart == mend: the first step's stage, then the closing pass at once)
+    assert np.max(np.abs(out["steps"][0] - H)) <= 1e-12 * hmax
+    np.testing.assert_allclose(out["steps"][1], Qg, rtol=0, atol=1e-11 * max(1.0, scale))
+    np.testing.assert_array_equal(out["native_steps"][0], out["steps"][0])
+    np.testing.assert_array_equal(out["native_steps"][1], out["steps"][1])
+
 
 def test_mgs2_icwy_solve_entry(gpu):
     """nkv_mgs_icwy_solve alone: x = (I + L)^{-1} b for a random row-major Gram matrix (the new row

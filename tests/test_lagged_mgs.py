@@ -112,6 +112,22 @@ def test_lagged_with_an_orthonormal_basis_is_mgs2():
     assert np.max(np.abs(G - np.eye(k + 1))) < 1e-12
 
 
+def test_lagged_in_one_column_calls_matches_one_call():
+    """The factorisation cut into calls of one, one, three and the remaining columns (each call
+    rebuilds the Gram rows, takes the first-step stage, and finishes its last column in the closing
+    pass) gives the single call's H and Q, from the unnormalised seed."""
+    A, w, q1 = _problem(seed=7)
+    n, k = q1.size, 20
+    Q1, H1 = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
+    Q2, H2 = np.zeros((n, k + 1)), np.zeros((k + 1, k), order="F")
+    Q1[:, 0] = Q2[:, 0] = q1
+    _lagged(A, w, Q1, H1, 0, k)
+    for c0, c1 in ((0, 1), (1, 2), (2, 5), (5, k)):
+        _lagged(A, w, Q2, H2, c0, c1)
+    assert np.max(np.abs(H2 - H1)) <= 1e-12 * np.max(np.abs(H1))
+    assert np.max(np.abs(Q2 - Q1)) <= 1e-11
+
+
 def test_lagged_flags_a_closed_krylov_space():
     """An operator of rank 3: the fourth column has no new direction.  Either the algebra raises the
     NaN error (r^2 <= 0) or H's subdiagonal collapses where krylov_schur's breakdown test
