@@ -108,4 +108,21 @@ def test_check_profile_groups_calls(tmp_path):
     kept = [line for line in txt.splitlines() if line.startswith("rotate kept")][0]
     assert kept.split()[2] == "1" and "(2 disp/call)" in kept and abs(float(kept.split()[-3]) - 1.0) < 1e-3, kept
     full = [line for line in txt.splitlines() if line.startswith("rotate full")][0]
-    assert full.split()[2] == "2" and abs(float(full.split()[-1]) - 1.0) < 1e-3, full
+    assert full.split()[2] == "2" and abs(float(full.split()[-3]) - 1.0) < 1e-3, full
+    # with the steady figure: the kept shape ran three times (the solver's call + two steady ones)
+    stats[2] = {"Name": ROTF, "Calls": "6", "TotalDurationNs": str(30 * ms)}
+    with open(tmp_path / "run_kernel_stats.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=["Name", "Calls", "TotalDurationNs"])
+        w.writeheader()
+        w.writerows(stats)
+    bench["restart"].update(rotate_kept_ms=11.4, rotate_kept_steady_ms=10.001)
+    bj.write_text(json.dumps(bench))
+    sys.argv = ["check_profile.py", str(tmp_path / "run_kernel_stats.csv"), str(bj)]
+    buf = io.StringIO()
+    try:
+        with redirect_stdout(buf):
+            cp.main()
+    finally:
+        sys.argv = old
+    kept = [line for line in buf.getvalue().splitlines() if line.startswith("rotate kept")][0]
+    assert kept.split()[2] == "3" and "(2 disp/call)" in kept and abs(float(kept.split()[-3]) - 1.0) < 1e-3, kept

@@ -65,38 +65,24 @@ def main():
           "event brackets include the ~5 us second-stage reduction kernel)")
     rs = bench.get("restart")
     if rs:
-        # restart rotations: n_out <= 16 kept columns (NKV_ROTF_MAX) run k_rotate_few<n_out, P, U>,
-        # wider ones k_rotate_stream<NB, MB, W, U> with MB = ceil(n_out / 16) column blocks
+        # restart rotations: n_out <= 16 kept columns (NKV_ROTF_MAX) run k_rotate_few<n_out, P, U>
+        # (one dispatch per row band), wider ones k_rotate_stream<NB, MB, W, U> with
+        # MB = ceil(n_out / 16) column blocks.  The kept shape runs 1 + 2 times (the solver's call,
+        # then rotate_kept_steady twice, back to back), the full one twice: per call, the profiler's
+        # summed kernel time over those calls, beside the steady event figure (the first call's
+        # extra is a one-time launch cost outside the kernels)
         n_kept = rs["mstart"] - 1
         kept_key = f"k_rotate_few<{n_kept}," if n_kept <= 16 else f"k_rotate_stream<1, {(n_kept + 15) // 16},"
-        # the kept shape runs three times (the solver's first-launch call, then twice steady): the
-        # trace's average is the kernels' own time, so it is set beside the steady event figure
-        for label, key, ms in (("rotate kept", kept_key, rs.get("rotate_kept_steady_ms", rs["rotate_kept_ms"])),
-                               ("rotate full", "k_rotate_stream<1, 8,", rs["rotate_full_ms"])):
-            if trace and key.startswith("k_rotate_few"):
-                # one call = a run of consecutive dispatches (the few-column rotation issues one per
-                # row band, NKV_ROTF_ROUNDS); its duration spans first start .. last end
-                spans, cur = [], None
-                for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
-                    if key in r["Kernel_Name"]:
-                        s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-                        cur = [s0, e0, 1] if cur is None else [cur[0], e0, cur[2] + 1]
-                    elif cur is not None:
-                        spans.append(cur)
-                        cur = None
-                if cur is not None:
-                    spans.append(cur)
-                if spans:
-                    avg = sum((e - s0) for s0, e, _ in spans) / len(spans) / 1e6
-                    print(f"{label:14s} {len(spans):13d} {avg:15.4f} {'':>16s} {ms:14.4f} {ms / avg:7.3f}"
-                          f"  ({spans[0][2]} disp/call)")
-                    continue
+        steady = "rotate_kept_steady_ms" in rs
+        for label, key, ms, ncall in (
+                ("rotate kept", kept_key, rs.get("rotate_kept_steady_ms", rs["rotate_kept_ms"]), 3 if steady else 1),
+                ("rotate full", "k_rotate_stream<1, 8,", rs["rotate_full_ms"], 2)):
             rows = [r for r in stats if key in r["Name"]]
             if rows:
-                calls = sum(int(r["Calls"]) for r in rows)
-                avg = sum(float(r["TotalDurationNs"]) for r in rows) / calls / 1e6
-                print(f"{label:14s} {calls:13d} {avg:15.4f} {'':>16s} {ms:14.4f} {ms / avg:7.3f}")
-
+                disp = sum(int(r["Calls"]) for r in rows)
+                avg = sum(float(r["TotalDurationNs"]) for r in rows) / ncall / 1e6
+                print(f"{label:14s} {ncall:13d} {avg:15.4f} {'':>16s} {ms:14.4f} {ms / avg:7.3f}"
+                      f"  ({disp // ncall} disp/call)")
 
 if __name__ == "__main__":
     main()
