@@ -16,6 +16,9 @@ typedef double nkv_f64x4 __attribute__((ext_vector_type(4)));
 #ifndef NKV_ROT_PIPE
 #define NKV_ROT_PIPE 1
 #endif
+#ifndef NKV_ROT_PIPE3_FROM
+#define NKV_ROT_PIPE3_FROM 5   // 16-column blocks from which two batches are kept ahead
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Restart rotation, streaming form (n_out <= 16*MB and V[:, 0:n_out] fits LDS): V is staged in
@@ -57,6 +60,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
                 for (int nb = 0; nb < NB; ++nb) b[u][nb] = i < k ? qi[nb * 16] : 0.0;
             }
         };
+        auto load_all = [&](double (&b)[U][NB], int i0) {   // a batch whose k-rows are all < k
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double* qi = q + (int64_t)(i0 + 4 * u + lk) * ld;
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) b[u][nb] = qi[nb * 16];
+            }
+        };
         auto mma = [&](const double (&b)[U][NB], int i0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -69,7 +80,34 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
                 }
             }
         };
-        if (NKV_ROT_PIPE) {   // the next batch's loads in flight while this batch's MFMAs issue
+        if (NKV_ROT_PIPE && MB >= NKV_ROT_PIPE3_FROM) {   // two batches ahead (wide column blocks: one
+            // wave per SIMD holds all of its MB accumulators, so its own loads must cover the latency)
+            double b0[U][NB], b1[U][NB], b2[U][NB];   // three batches per trip: no register copies
+            load(b0, 0);
+            if (4 * U < k) load(b1, 4 * U);
+            int i0 = 0;
+            // steady trips: every k-row of the batches loaded here is < k, so the loads carry no
+            // per-lane guard (a guarded load is an exec-masked branch, after which the compiler
+            // waits with vmcnt(0), for every load in flight, instead of for the batch it needs)
+            for (; i0 + 20 * U <= k; i0 += 12 * U) {   // b0, b1: batches i0, i0+4U; i0+8U..i0+16U whole
+                load_all(b2, i0 + 8 * U);
+                mma(b0, i0);
+                load_all(b0, i0 + 12 * U);
+                mma(b1, i0 + 4 * U);
+                load_all(b1, i0 + 16 * U);
+                mma(b2, i0 + 8 * U);
+            }
+            // b0 holds the batch at i0 < k, b1 the one at i0+4U when it exists: the rest, guarded
+            for (;; i0 += 8 * U) {   // wave-uniform branches
+                mma(b0, i0);
+                if (i0 + 4 * U >= k) break;
+                const bool more2 = i0 + 8 * U < k;
+                if (more2) load(b0, i0 + 8 * U);
+                mma(b1, i0 + 4 * U);
+                if (!more2) break;
+                if (i0 + 12 * U < k) load(b1, i0 + 12 * U);
+            }
+        } else if (NKV_ROT_PIPE) {   // the next batch's loads in flight while this batch's MFMAs issue
             double b0[U][NB], b1[U][NB];   // two batches per trip: no register copies
             load(b0, 0);
             for (int i0 = 0;; i0 += 8 * U) {   // b0 holds the batch at i0 < k (wave-uniform branches)

@@ -141,15 +141,12 @@ VARIANTS = {
     # pipeline: twice the bytes in flight per wave at one wave per SIMD); the multi-dot is the
     # box-sensitive kernel (6.55-6.79 TB/s across boxes, the dual update 6.97-7.02)
     "d2_pf": {"patch": "d2_prefetch"},
-    # round 5: the streaming MFMA rotation (17-128 kept columns, 0.63 of HBM at 26-32 kept) was meant
-    # to hold the next batch's loads in flight during this batch's MFMAs, but its loads sit under
-    # wave-uniform branches and the compiler waits with vmcnt(0) — for every load in flight.  The
-    # steady loop with unconditional loads (2 batches, or 3: two ahead), and 8-wave workgroups
-    # (3 per CU at 74-82 VGPRs: 24 waves per CU instead of 16)
-    "rot_unc": {"patch": "rot_uncond"},
-    "rot_unc3": {"patch": "rot_uncond3"},
-    "rot_unc_w8": {"NKV_ROT_WAVES": 8, "patch": "rot_uncond"},
-    "rot_unc3_w8": {"NKV_ROT_WAVES": 8, "patch": "rot_uncond3"},
+    # round 5: the streaming MFMA rotation's pipeline sat behind guarded (exec-masked) loads, after
+    # which the compiler waits with vmcnt(0) for every load in flight: unguarded steady-state loads
+    # with two batches ahead, adopted from 5 column blocks (one wave per SIMD; +9-13 % at 65-128
+    # kept columns, r05aj), no change at 17-64 (r05ai, whose experiment patches were retired)
+    "rot_p3_off": {"NKV_ROT_PIPE3_FROM": 99},   # the rotation before r05aj
+    "rot_p3_from4": {"NKV_ROT_PIPE3_FROM": 4},
 }
 
 
