@@ -8,7 +8,7 @@ import os
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 PROF = os.path.join(ROOT, "profiles")
-LATEST = "r05ah"
+LATEST = "r05ak"
 KEY = {"dcgs2_update": "k_dcgs2_update<", "block_dot2": "k_block_dot2<"}
 
 
