@@ -34,7 +34,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     dev = torch.device("cuda", 0)
     bad = 0
-    for k, n_out in ((128, 128), (128, 20), (128, 64), (37, 33), (200, 17), (96, 96), (150, 40)):
+    for k, n_out in ((128, 128), (128, 20), (128, 64), (37, 33), (200, 17), (96, 96), (150, 40),
+                     (200, 100), (200, 200), (257, 129), (1000, 40)):
         outs = []
         V = torch.as_tensor(np.random.default_rng(k * 1000 + n_out).standard_normal((n_out, k))).to(dev)
         for L in libs:

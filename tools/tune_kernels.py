@@ -147,6 +147,10 @@ VARIANTS = {
     # kept columns, r05aj), no change at 17-64 (r05ai, whose experiment patches were retired)
     "rot_p3_off": {"NKV_ROT_PIPE3_FROM": 99},   # the rotation before r05aj
     "rot_p3_from4": {"NKV_ROT_PIPE3_FROM": 4},
+    # the k-chunked rotation (V not in LDS whole: k = 200 beyond 80 kept columns, or > 128 kept)
+    # has the same guarded loads: the steady chunks with unguarded ones are bit-identical but
+    # 12-55 % slower at k = 160-200 (r05al): not adopted
+    "rot_chunk_unc": {"patch": "rot_chunk_unc"},
 }
 
 
