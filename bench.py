@@ -234,7 +234,8 @@ def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_f
                               else "4-pass CGS2 with fused norm + matvec (SURVEY.md 8(d) B(j), bench.survey_model_bytes)"),
         seconds_per_factorisation_sample=round(sec_fact, 3),
         seconds_per_factorisation_measured=True,
-        seconds_per_factorisation_N1e8=round(sec_fact * scale, 2),
+        E_sample=E_sample,
+        seconds_scaled_from_sample_N1e8=round(sec_fact * scale, 2),
         step_seconds={int(j): round(float(t_step[j - 1]), 4) for j in sorted(set(js + [m]))},
         fit_check={"js": js, "fitted_total_s": round(fit_total, 3),
                    "rel_err_vs_measured": round((fit_total - sec_fact) / sec_fact, 4)},
@@ -244,27 +245,104 @@ def cpu_baseline(E_sample: int, m: int, threads: int, variant: str = "mgs2", n_f
                 + f"; {threads} thread(s) on {cpu_model()}"))
 
 
-def cpu_full_size_run(E: int, m: int, gpu_ms_per_step: float):
+FULL_SIZE_FILES = {"mgs2": "cpu_full_size_latest.json", "cgs2": "cpu_full_size_cgs2_latest.json"}
+
+
+def cpu_full_size_run(E: int, m: int, gpu_ms_per_step: float, variant: str = "mgs2", threads: int | None = None):
     """The same CPU factorisation measured ONCE at full size on the GPU box's host, outside this run
-    (``tools/cpu_factorisation.py <out> <E>``, ~9 min at N=1e8, too long for the bench's own sample):
-    read from ``profiles/cpu_full_size_latest.json`` when it matches this workload, else None.
-    It checks the N-scaling of the bounded sample above; it is never ``value``."""
-    path = os.path.join(ROOT, "profiles", "cpu_full_size_latest.json")
+    (``tools/cpu_factorisation.py <out> <E> [--variant cgs2]``, minutes at N=1e8, too long for the
+    bench's own sample): read from ``profiles/cpu_full_size_latest.json`` (the reference MGS2) or
+    ``profiles/cpu_full_size_cgs2_latest.json`` (the optimised CPU CGS2) when it matches this
+    workload (E, m) and, if given, this host's thread count; else None.  It is never ``value``."""
+    path = os.path.join(ROOT, "profiles", FULL_SIZE_FILES[variant])
     if not os.path.exists(path):
         return None
     try:
         fj = json.load(open(path))
         r = fj["runs"][0]
-        if r.get("E") != E or fj.get("m") != m:
+        if r.get("E") != E or fj.get("m") != m or (threads is not None and int(r["cores"]) != int(threads)):
             return None
         s = float(r["seconds_per_factorisation_sample"])
         return {"seconds_per_factorisation": s, "E": r["E"], "threads": r["cores"], "kind": r["kind"],
-                "file": "profiles/cpu_full_size_latest.json", "collected": fj.get("tag"), "head": fj.get("head"),
+                "file": "profiles/" + FULL_SIZE_FILES[variant], "collected": fj.get("tag"), "head": fj.get("head"),
+                "cpu": (fj.get("host") or {}).get("cpu"),
                 "time_to_solution_ratio_cpu_over_gpu": round(s / (gpu_ms_per_step * 1e-3), 1),
                 "note": "measured separately on the GPU box's host (not in this run): one complete "
-                        "factorisation of the reference MGS2 restatement at this N"}
+                        "factorisation of this CPU algorithm at this N"}
     except (OSError, ValueError, KeyError, IndexError, TypeError):
         return None
+
+
+def lead_with_measured(c: dict, full: dict | None, gpu_ms: float) -> dict:
+    """The seconds-to-solution at N=1e8 and the CPU/GPU time ratio come from a measurement: the
+    full-size run when one exists for this algorithm, workload and thread count.
+    The bounded sample's N-scaled figure stays beside it as ``seconds_scaled_from_sample_N1e8`` with
+    its error against the measurement; without a full-size run the ratio is reported only as an
+    ``..._estimate`` and ``seconds_per_factorisation_N1e8`` is null."""
+    c["gpu_ms_per_factorisation"] = round(gpu_ms, 2)
+    c["full_size_run"] = full
+    scaled = c["seconds_scaled_from_sample_N1e8"]
+    if full is not None:
+        s = full["seconds_per_factorisation"]
+        c["seconds_per_factorisation_N1e8"] = s
+        c["seconds_per_factorisation_N1e8_source"] = (f"measured at full size, E={full['E']}, {full['threads']} "
+                                                      f"threads ({full['file']}, {full['collected']})")
+        c["time_to_solution_ratio_cpu_over_gpu"] = round(s / (gpu_ms * 1e-3), 1)
+        c["sample_scaled_over_measured"] = round(scaled / s, 3)
+    else:
+        c["seconds_per_factorisation_N1e8"] = None
+        c["seconds_per_factorisation_N1e8_source"] = "not measured at full size for this algorithm / thread count"
+        c["time_to_solution_ratio_cpu_over_gpu"] = None
+        c["time_to_solution_ratio_estimate"] = round(scaled / (gpu_ms * 1e-3), 1)
+        c["estimate_note"] = ("the bounded sample scaled linearly in N (an estimate; for the reference MGS2 on 16 "
+                              "threads that scaling over-stated the full-size measurement by ~19-30 %)")
+    return c
+
+
+PORT_NOTE = ("the C port runs up to ~1.7x slower than the reference's own Fortran did in the survey's "
+             "single-core probe (E=2000, m=16: 7.1 s vs 4.215 s; CHANGELOG.md round 3), so the CPU time "
+             "may over-state the reference's by up to that factor")
+
+
+def host_baselines(args, m: int, gpu_ms: float) -> dict:
+    """The three CPU lines timed live on this host (rank 0 only, after every rank has left the
+    process group at world > 1, so no peer waits in a collective meanwhile), each led by its
+    measured full-size figures where they exist."""
+    host = host_threads()
+    cpu = cpu_baseline(args.cpu_E, m, host["threads"])
+    cpu1 = cpu_baseline(args.cpu_E_1core, m, 1)
+    cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], variant="cgs2")
+    lead_with_measured(cpu, cpu_full_size_run(args.E, m, gpu_ms, "mgs2", host["threads"]), gpu_ms)
+    lead_with_measured(cpu1, cpu_full_size_run(args.E, m, gpu_ms, "mgs2", 1), gpu_ms)
+    lead_with_measured(cpu_opt, cpu_full_size_run(args.E, m, gpu_ms, "cgs2", host["threads"]), gpu_ms)
+    cpu["host"] = host
+    for c in (cpu, cpu1):
+        c["sample"] += "; " + PORT_NOTE
+    return {"cpu_baseline": cpu, "cpu_baseline_1core": cpu1, "cpu_optimised": cpu_opt}
+
+
+def find_traffic(dom: str, E_shard: int, m: int):
+    """PMC HBM bytes per launch of the dominant kernel family for a rank whose shard holds
+    ``E_shard`` elements: ``profiles/traffic_latest.json`` (the full one-GPU size) or
+    ``profiles/traffic_E<E>.json`` (a shard size measured alone on one GPU: the same per-launch
+    bytes a rank of that shard moves at world > 1).  Returns (bytes, provenance) or (None, None)."""
+    import glob
+
+    paths = [os.path.join(ROOT, "profiles", "traffic_latest.json")]
+    paths += sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_E*.json")))
+    for path in paths:
+        try:
+            tj = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if tj.get("kernel_family") == dom and tj.get("E") == E_shard and tj.get("m") == m:
+            return tj.get("hbm_bytes_per_launch"), {
+                "file": os.path.relpath(path, ROOT), "collected": tj.get("tag") or tj.get("source"),
+                "box": tj.get("box"), "head": tj.get("head"), "E_shard": E_shard,
+                "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate passes, "
+                          "tools/pmc_traffic.py; one GPU running a shard of this size alone; not collected in "
+                          "this run"}
+    return None, None
 
 
 # ---- launcher ----------------------------------------------------------------------------------
@@ -356,6 +434,9 @@ def parse_args(argv=None):
                     help="at one GPU, route every partial through a world-1 RCCL group (collective cost)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print each rank's launch environment and stop before GPU initialisation")
+    ap.add_argument("--dry-line", action="store_true",
+                    help="CPU rehearsal of the JSON line at any world size: gloo ranks, fabricated (labelled) "
+                         "measurements, the real line assembly and the real rank-0 CPU baselines")
     ap.add_argument("--collective-probe", action="store_true",
                     help="CPU test of the collective path: init the process group (bounded timeout, rank "
                          "watchdog), gather the ranks' device identities, one all-reduce, print one JSON line")
@@ -393,7 +474,10 @@ def main():
     sys.stdout.flush()
     args.json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    run(args)
+    if args.dry_line:
+        run_dry_line(args)
+    else:
+        run(args)
 
 
 # ---- one rank ----------------------------------------------------------------------------------
@@ -430,18 +514,19 @@ def collective_probe() -> int:
     return 0
 
 
-def _leave_group(comm) -> None:
+def _leave_group(comm, keep_rank0: bool = False) -> None:
     """Every rank leaves the process group together, then the process ends without the
     interpreter's teardown: c10d's background threads, torn down by static destructors at exit, were
     seen to abort a gloo rank ("terminate called without an active exception", status -6) after its
-    work was done — which a launcher reports as a failed job."""
+    work was done — which a launcher reports as a failed job.  ``keep_rank0``: rank 0 returns (it
+    still has host work to do and ends with ``os._exit`` itself)."""
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()):
         return
     comm.barrier()
     dist.destroy_process_group()
-    if comm.world > 1:
+    if comm.world > 1 and not (keep_rank0 and comm.rank == 0):
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(0)
@@ -628,6 +713,17 @@ def run(args):
     else:
         del d_scaled
 
+    out = bench_line(args, comm, glay, lay, m, elapsed, phases, last_step_ms, vals, res, exact, restart, ks_leg,
+                     ks_restart, devices, dev)
+    finish(args, comm, out, m)
+
+
+def bench_line(args, comm, glay, lay, m, elapsed, phases, last_step_ms, vals, res, exact, restart, ks_leg,
+               ks_restart, devices, dev):
+    """The ONE JSON line from the measurements (rank 0's copy is printed; the *_over_ranks figures are
+    collectives, so every rank calls this).  The CPU lines are attached by ``finish`` after every
+    rank has left the process group."""
+    world = comm.world
     ms_per_step = elapsed / args.steps * 1e3
     nv_g = glay.pts_v * glay.nelgv
     exec_b = executed_bytes(glay.N, glay.N_w, nv_g, m, args.mode)
@@ -680,99 +776,119 @@ def run(args):
     # kernel-family events in those modes (their kernels are in a rocprof trace), only `value`
     ph = phases.get(dom, {"gbps": 0.0, "avg_ms": 0.0, "avg_bytes": 0.0, "launches": 0})
     achieved = ph["gbps"]
-    traffic, tsrc = None, None
-    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if tj.get("kernel_family") == dom and tj.get("E") == args.E and tj.get("m") == m and world == 1:
-                traffic = tj.get("hbm_bytes_per_launch")
-                tsrc = {"file": "profiles/traffic_latest.json", "collected": tj.get("tag") or tj.get("source"),
-                        "box": tj.get("box"), "head": tj.get("head"),
-                        "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate "
-                                  "passes, tools/pmc_traffic.py; not collected in this run"}
-        except Exception:  # noqa: BLE001
-            traffic = None
+    traffic, tsrc = find_traffic(dom, lay.nelv, m)
 
-    if rank == 0:
-        cpu = cpu1 = cpu_opt = host = None
-        if not args.no_cpu and world == 1:
-            host = host_threads()
-            cpu = cpu_baseline(args.cpu_E, m, host["threads"])
-            cpu1 = cpu_baseline(args.cpu_E_1core, m, 1)
-            cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], variant="cgs2")
-            for c in (cpu, cpu1, cpu_opt):
-                # the comparison to lead with: wall time of the same factorisation (different
-                # algorithms move different bytes, so GB/s ratios are not work ratios)
-                c["time_to_solution_ratio_cpu_over_gpu"] = round(c["seconds_per_factorisation_N1e8"] /
-                                                                 (ms_per_step * 1e-3), 1)
-                c["gpu_ms_per_factorisation"] = round(ms_per_step, 2)
-            cpu["host"] = host
-            cpu["full_size_run"] = cpu_full_size_run(args.E, m, ms_per_step)
-        out = {
-            "metric": "Arnoldi-step GB/s (achieved HBM) + Ritz-value rel-err, N=1e8 m=128",
-            "value": round(value, 2),
+    out = {
+        "metric": "Arnoldi-step GB/s (achieved HBM) + Ritz-value rel-err, N=1e8 m=128",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "world": world,
+        "backend": comm.backend if world > 1 or args.force_collectives else None,
+        "devices": devices,
+        "distinct_devices": distinct_devices(devices),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "survey_model_time_ratio": round(survey_time_ratio, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (diagonalised shift-invert Laplacian, hashed seed, GLL x J_e weights)",
+        "config": {
+            "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
+            "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
+            "m": m, "mode": args.mode,
+            "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
+                            + " allreduce") if world > 1 else "single GPU",
+        },
+        "roofline": None if dom not in phases else {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "n_gpus": world,
-            "world": world,
-            "backend": comm.backend if world > 1 or args.force_collectives else None,
-            "devices": devices,
-            "distinct_devices": distinct_devices(devices),
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "survey_model_time_ratio": round(survey_time_ratio, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (diagonalised shift-invert Laplacian, hashed seed, GLL x J_e weights)",
-            "config": {
-                "workload": f"config3: m-step Arnoldi ({args.mode.upper()}) + Ritz extraction, shift-invert Laplacian",
-                "N": glay.N, "N_w": glay.N_w, "E": args.E, "layout": "3D lx1=8 lx2=6 {vx,vy,vz,t}+pr",
-                "m": m, "mode": args.mode,
-                "parallelism": (f"element-shard x{world} + " + ("RCCL" if comm.backend == "nccl" else str(comm.backend))
-                                + " allreduce") if world > 1 else "single GPU",
-            },
-            "roofline": None if dom not in phases else {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": tsrc,
-                "launch": ("one entry-point call per Arnoldi step (nkv_dcgs2_update: NKV_DC_ROUNDS row-band "
-                           "dispatches; events span all of them)" if dom == "dcgs2_update" else "one entry-point call"),
-                "avg_launch_ms": round(ph["avg_ms"], 4),
-                "avg_bytes_per_launch": ph["avg_bytes"],
-                "launches": ph["launches"],
-                "scope": "one GPU (the only rank)" if world == 1 else
-                         f"rank 0's shard on its own GPU (1/{world} of N); peak is one GPU's HBM",
-                # a rank's vector that fits the 256 MiB Infinity Cache (MALL) is partly re-read from
-                # it (the vector one kernel writes is read by the next): not pure HBM traffic
-                "infinity_cache": (None if 8.0 * lay.ld >= 256 * 2 ** 20 else
-                                   f"rank vectors of {8.0 * lay.ld / 2 ** 20:.0f} MiB fit the 256 MiB Infinity "
-                                   "Cache: part of the achieved rate is MALL hits, not HBM"),
-            },
-            "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                       for k, v in phases.items()},
-            "gram_schmidt": gs,
-            "ritz_rel_err": ritz_err,
-            "ritz_top8_rel_err": top_err,
-            "ritz_converged": int(conv.sum()),
-            "ritz_top8": [[float(v.real), float(v.imag)] for v in vals[:8]],
-            "cpu_baseline": cpu,
-            "cpu_baseline_1core": cpu1,
-            "cpu_optimised": cpu_opt,
-            "restart": restart,
-            "krylov_schur_leg": ks_leg,
-            "krylov_schur_restart_leg": ks_restart,
-        }
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "launch": ("one entry-point call per Arnoldi step (nkv_dcgs2_update: NKV_DC_ROUNDS row-band "
+                       "dispatches; events span all of them)" if dom == "dcgs2_update" else "one entry-point call"),
+            "avg_launch_ms": round(ph["avg_ms"], 4),
+            "avg_bytes_per_launch": ph["avg_bytes"],
+            "launches": ph["launches"],
+            "scope": "one GPU (the only rank)" if world == 1 else
+                     f"rank 0's shard on its own GPU (1/{world} of N); peak is one GPU's HBM",
+            # a rank's vector that fits the 256 MiB Infinity Cache (MALL) is partly re-read from
+            # it (the vector one kernel writes is read by the next): not pure HBM traffic
+            "infinity_cache": (None if 8.0 * lay.ld >= 256 * 2 ** 20 else
+                               f"rank vectors of {8.0 * lay.ld / 2 ** 20:.0f} MiB fit the 256 MiB Infinity "
+                               "Cache: part of the achieved rate is MALL hits, not HBM"),
+        },
+        "phases": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                   for k, v in phases.items()},
+        "gram_schmidt": gs,
+        "ritz_rel_err": ritz_err,
+        "ritz_top8_rel_err": top_err,
+        "ritz_converged": int(conv.sum()),
+        "ritz_top8": [[float(v.real), float(v.imag)] for v in vals[:8]],
+        "cpu_baseline": None,
+        "cpu_baseline_1core": None,
+        "cpu_optimised": None,
+        "restart": restart,
+        "krylov_schur_leg": ks_leg,
+        "krylov_schur_restart_leg": ks_restart,
+    }
+    return out
+
+
+def finish(args, comm, out, m) -> None:
+    """Every rank leaves the process group together; the ranks other than 0 end there.  Rank 0 then
+    times the CPU lines (unless --no-cpu) — at every world size, with no peer left waiting in a
+    collective — and prints the ONE JSON line."""
+    rank, world = comm.rank, comm.world
+    _leave_group(comm, keep_rank0=True)
+    if rank == 0:
+        if not args.no_cpu:
+            out.update(host_baselines(args, m, out["ms_per_step"]))
         print(json.dumps(out), file=args.json_out, flush=True)
     args.json_out.flush()
-    _leave_group(comm)   # every rank leaves the RCCL group before the process exits
+    if world > 1:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+
+def run_dry_line(args) -> None:
+    """``--dry-line``: the multi-rank line assembly without a GPU (CPU test of the N > 1 contract).
+    Every rank joins a gloo group and contributes fabricated, clearly labelled measurements of the
+    right shape (phases of the DCGS2 kernel families, step time, Ritz values); the line is built by
+    the same ``bench_line`` and finished by the same ``finish`` (CPU lines on rank 0 after the group
+    is left) as a real run, so its keys are the real line's keys."""
+    from nekstab_next_amd.comm import init_from_env
+    from nekstab_next_amd.layout import box3d_layout
+
+    comm = init_from_env("gloo")
+    devices = comm.devices()
+    glay = box3d_layout(args.E)
+    lay = glay.shard(comm.rank, comm.world)
+    m = args.m
+    n1 = 8.0 * ((m - 1) * lay.N_w + 2 * lay.N_w + lay.n_v)
+    n2 = 8.0 * ((m - 1) * lay.N + 4 * lay.N)
+    phases = {"block_dot2": dict(launches=m * args.steps, total_ms=1.0 * m * args.steps, avg_ms=1.0, avg_bytes=n1,
+                                 gbps=n1 / 1e-3 / 1e9),
+              "dcgs2_update": dict(launches=m * args.steps, total_ms=1.1 * m * args.steps, avg_ms=1.1, avg_bytes=n2,
+                                   gbps=n2 / 1.1e-3 / 1e9)}
+    if comm.world > 1:
+        phases["allreduce"] = dict(launches=m * args.steps, total_ms=0.01 * m * args.steps, avg_ms=0.01,
+                                   avg_bytes=16.0 * m, gbps=0.0)
+    exact = np.linspace(2.0, 1.0, max(m, 8))
+    vals = exact.astype(complex)
+    res = np.full(vals.shape, 1e-9)
+    elapsed = comm.max_scalar(2.5 * m * 1e-3 * args.steps)
+    out = bench_line(args, comm, glay, lay, m, elapsed, phases, 2.1, vals, res, exact, None, None, None, devices, None)
+    out["dry_line"] = "fabricated measurements (CPU rehearsal of the line's shape); not a result"
+    finish(args, comm, out, m)
 
 
 if __name__ == "__main__":

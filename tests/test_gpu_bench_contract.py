@@ -81,8 +81,9 @@ def test_bench_json_contract(gpu):
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
-    assert cb["cores"] == cb["host"]["threads"] and cb["seconds_per_factorisation_N1e8"] > 0
-    assert cb["time_to_solution_ratio_cpu_over_gpu"] > 1
+    assert cb["cores"] == cb["host"]["threads"] and cb["seconds_scaled_from_sample_N1e8"] > 0
+    # E=2000 is not BASELINE's workload: no full-size CPU measurement applies, the ratio is an estimate
+    assert cb["seconds_per_factorisation_N1e8"] is None and cb["time_to_solution_ratio_estimate"] > 1
     _one_byte_model(d)
     assert d["world"] == 1 and d["gram_schmidt"]["allreduce_ms_per_factorisation"] == 0
     assert len(d["devices"]) == 1 and d["devices"][0]["pci"] and d["distinct_devices"] is True

@@ -41,18 +41,56 @@ def _write_pmc(path, seq):
 
 def test_pmc_traffic_sums_band_dispatches_per_call(tmp_path):
     pt = _tool("pmc_traffic")
+    lm = _tool("launch_model")
+    rows = 4608 * 4096   # 3 row bands of the DCGS2 update, 12 of the few-column rotation
+    assert lm.dispatches_per_call(UPD, rows) == 3 and lm.dispatches_per_call(ROTF, rows) == 12
     # two DCGS2 steps: dot2 + its reduction, coef, then the update as 3 band dispatches
     seq = []
     for _ in range(2):
         seq += [(DOT2, 10.0), (RED, 0.5), (COEF, 0.1), (UPD, 1.0), (UPD, 2.0), (UPD, 3.0)]
-    seq += [(ROTF, 4.0), (ROTF, 4.0)]   # one banded restart rotation (2 dispatches)
+    seq += [(ROTF, 4.0)] * 12   # one banded restart rotation (12 dispatches)
     d = tmp_path / "p"
     d.mkdir()
     _write_pmc(d / "run_counter_collection.csv", seq)
-    out = pt.load(str(d))
+    out = pt.load(str(d), rows)
     assert out["dcgs2_update"] == [(6.0, 3), (6.0, 3)]       # k_reduce_cols/coef do not merge steps
     assert out["block_dot2"] == [(10.0, 1), (10.0, 1)]       # not banded: one dispatch per call
-    assert out["rotate_kept"] == [(8.0, 2)]
+    assert out["rotate_kept"] == [(48.0, 12)]
+
+
+def test_pmc_traffic_splits_back_to_back_calls(tmp_path):
+    """bench.py's restart leg calls the kept-column rotation three times back to
+    back; grouping by adjacency merged them (a phantom x1.5 over-fetch).  Calls are now counted off
+    by the entry point's band count at the layout."""
+    pt = _tool("pmc_traffic")
+    rows = 4608 * 4096
+    seq = [(ROTF, 1.0)] * 36 + [(UPD, 2.0)] * 6   # three rotations, then two dual updates, all adjacent
+    d = tmp_path / "p"
+    d.mkdir()
+    _write_pmc(d / "run_counter_collection.csv", seq)
+    out = pt.load(str(d), rows)
+    assert out["rotate_kept"] == [(12.0, 12)] * 3
+    assert out["dcgs2_update"] == [(6.0, 3)] * 2
+
+
+def test_launch_model_matches_committed_traces():
+    """The band counts the model derives for bench.py's layout (E=44,176) divide the dispatch counts
+    of a committed full-size rocprofv3 trace into whole calls: the dual update and the diagonal
+    matvec once per Arnoldi step (as many calls as multi-dots), the 6-kept rotation 3 times."""
+    lm = _tool("launch_model")
+    rows = lm.rows_of_E(44176)
+    calls = {}
+    with open(os.path.join(ROOT, "profiles", "r05ak_bench_n1_kernel_stats.csv")) as fh:
+        for r in csv.DictReader(fh):
+            calls[r["Name"]] = int(r["Calls"])
+    n = {k: v for k, v in calls.items()}
+    upd = next(k for k in n if "k_dcgs2_update<8, false>" in k)
+    opd = next(k for k in n if "k_op_diag(" in k)
+    rotf = next(k for k in n if "k_rotate_few<6, 4, 4>" in k)
+    dot2 = next(k for k in n if "k_block_dot2<8>" in k)
+    assert n[upd] == lm.dispatches_per_call(upd, rows) * n[dot2] == 16 * n[dot2]
+    assert n[opd] == lm.dispatches_per_call(opd, rows) * n[dot2] == 6 * n[dot2]
+    assert n[rotf] == 3 * lm.dispatches_per_call(rotf, rows) == 3 * 64
 
 
 def _write_trace(path, seq):

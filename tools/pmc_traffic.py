@@ -16,6 +16,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import launch_model  # noqa: E402
+
 FAMILIES = {
     "block_dot": ("k_block_dot<",),
     "block_dot2": ("k_block_dot2<",),
@@ -25,37 +28,52 @@ FAMILIES = {
     "finish": ("k_finish",),
     "op_diag": ("k_op_diag",),
     "copy": ("k_blas1<1>",),
-    # restart rotations of bench.py's restart leg (k_rotate_few: 16 B/lane loads; k_rotate_stream:
-    # 8 B/lane loads, so its rows show how far the x2 FETCH correction holds for narrower loads)
-    "rotate_kept": ("k_rotate_few<", "k_rotate_stream<1, 1,"),
+    # restart rotations of bench.py's restart leg: <= 16 kept columns (k_rotate_few, 16 B/lane loads),
+    # 17-64 kept (k_rotate_wide, 16 B/lane; k_rotate_stream<1, 2..4 before round 6, 8 B/lane) and the
+    # full k-column rotation (k_rotate_stream<1, 8,: 8 B/lane loads, where the x2 FETCH correction is
+    # uncalibrated)
+    "rotate_kept": ("k_rotate_few<",),
+    "rotate_wide": ("k_rotate_wide<", "k_rotate_stream<1, 2,", "k_rotate_stream<1, 3,", "k_rotate_stream<1, 4,"),
     "rotate_full": ("k_rotate_stream<1, 8,",),
 }
 
 
-BANDED = ("dcgs2_update", "op_diag", "rotate_kept")  # families whose entry points issue row-band dispatches
-
-
-def load(d):
+def load(d, rows, counter=None):
     """Per-CALL counter values per family.  One entry-point call may issue several dispatches back
     to back (the row bands of the DCGS2 update, NKV_DC_ROUNDS; of the diagonal matvec,
-    NKV_STREAM_ROUNDS; of the few-column restart rotation, NKV_ROTF_ROUNDS): a call = a run of
-    consecutive dispatches of one family in dispatch order (k_reduce_cols, the second reduction
-    stage, does not end a run); its value is their sum."""
-    rows = sorted(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))),
-                  key=lambda r: int(r["Dispatch_Id"]))
-    out = collections.defaultdict(list)
-    cur_fam, cur = None, None
-    for r in rows:
-        fam = fam_of(r["Kernel_Name"])
-        if fam is not None and fam == cur_fam and fam in BANDED:
-            cur[0] += float(r["Counter_Value"])
-            cur[1] += 1
+    NKV_STREAM_ROUNDS; of the few-column restart rotation, NKV_ROTF_ROUNDS), and the bench calls
+    some entry points back to back (the restart leg's three kept-column rotations).  A call is
+    therefore the number of dispatches the entry point issues at this layout
+    (tools/launch_model.dispatches_per_call, from the kernel instantiation and ``rows``), counted
+    off consecutive dispatches of the family; k_reduce_cols (the second reduction stage) is
+    skipped; its value is their sum."""
+    kn = launch_model.knobs()
+    disp = {}   # dispatch id -> [kernel name, counter value summed over the dispatch's rows]
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if counter is not None and r["Counter_Name"] != counter:
             continue
-        if fam is None and "k_reduce_cols" in r["Kernel_Name"]:
+        e = disp.setdefault(int(r["Dispatch_Id"]), [r["Kernel_Name"], 0.0])
+        e[1] += float(r["Counter_Value"])
+    out = collections.defaultdict(list)
+    cur_fam, cur, left = None, None, 0
+    for did in sorted(disp):
+        name, value = disp[did]
+        fam = fam_of(name)
+        if fam is None and "k_reduce_cols" in name:
+            continue
+        if fam is not None and fam == cur_fam and left > 0:
+            cur[0] += value
+            cur[1] += 1
+            left -= 1
             continue
         if cur_fam is not None:
             out[cur_fam].append(tuple(cur))
-        cur_fam, cur = fam, ([float(r["Counter_Value"]), 1] if fam is not None else None)
+        cur_fam = fam
+        if fam is not None:
+            cur = [value, 1]
+            left = launch_model.dispatches_per_call(name, rows, kn) - 1
+        else:
+            cur, left = None, 0
     if cur_fam is not None:
         out[cur_fam].append(tuple(cur))
     return out
@@ -71,8 +89,9 @@ def fam_of(name):
 def main():
     fdir, wdir, bench_json, out_json = sys.argv[1:5]
     opt = dict(zip(sys.argv[5::2], sys.argv[6::2]))
-    F, W = load(fdir), load(wdir)
     bench = json.load(open(bench_json))
+    rows = launch_model.rows_of_E(bench["config"]["E"])
+    F, W = load(fdir, rows, "FETCH_SIZE"), load(wdir, rows, "WRITE_SIZE")
     agg = {}
     for fam in FAMILIES:
         fv = [v for v, _ in F.get(fam, [])]
