@@ -99,14 +99,18 @@ def executed_bytes(N, N_w, n_v, m, mode):
             tot += dot + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
         elif mode == "mgs2-icwy":   # two-vector dot (Gram row + pass-1 dots), fused update+dot, update+norm
             tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v) + (upd + 8.0 * n_v) + (upd + 8.0 * n_v)
-        elif mode == "dcgs2":   # two-vector dot over j-1 streamed columns (+ u, A u); dual update over j-1
+        elif mode in ("dcgs2", "mgs2-lagged"):   # two-vector dot over j-1 streamed columns (+ u, A u); dual
+            # update over j-1 (mgs2-lagged: the same two kernels with MGS2's coefficients from the host)
             tot += 8.0 * ((j - 1) * N_w + 2 * N_w + n_v)
             tot += 8.0 * ((j - 1) * N + 4 * N)
         else:
             raise ValueError(mode)
-        tot += (0.0 if mode == "dcgs2" else 8.0 * 2 * N) + 8.0 * 3 * N   # normalise pass (not in dcgs2) + matvec
-    if mode == "dcgs2":  # closing re-orthogonalisation of q_{m+1}: dot, update, normalise
+        tot += (0.0 if mode in ("dcgs2", "mgs2-lagged") else 8.0 * 2 * N) + 8.0 * 3 * N   # normalise (not
+        # in the delayed forms) + matvec
+    if mode in ("dcgs2", "mgs2-lagged"):  # closing re-orthogonalisation of q_{m+1}: dot, update, normalise
         tot += 8.0 * ((m + 1) * N_w + N_w + n_v) + 8.0 * (m * N + 2 * N) + 8.0 * 2 * N
+        if mode == "mgs2-lagged":   # its closing update carries the fused norm (the weights once more)
+            tot += 8.0 * n_v
     return tot
 
 
@@ -423,7 +427,9 @@ def parse_args(argv=None):
     ap.add_argument("--m", type=int, default=128)
     ap.add_argument("--mode", default="dcgs2",
                     help="dcgs2 (default) | cgs2 | mgs2 (reference order) | dcgs2-native | "
-                         "cgs2-native | mgs2-native (the one-call C drivers) | mgs2-icwy (MGS in inverse compact WY form)")
+                         "cgs2-native | mgs2-native (the one-call C drivers) | mgs2-icwy (MGS in inverse compact WY form) "
+                         "| mgs2-lagged[-native] (MGS2's coefficients, second pass lagged: the non-orthonormal-seed "
+                         "default)")
     ap.add_argument("--cpu-E", type=int, default=2000,
                     help="CPU baseline sample: one full factorisation on all threads (2,000 -> N=4.5e6, ~20 s)")
     ap.add_argument("--cpu-E-1core", type=int, default=128, help="... with one thread (128 -> N=2.9e5)")
@@ -650,7 +656,8 @@ def run(args):
     ctx.timer = None
     comm.timer = None
     phases = timer.summary()
-    last_step_ms = sum(timer.last_ms(k) for k in ("block_dot2", "dcgs2_update")) if args.mode == "dcgs2" else None
+    last_step_ms = (sum(timer.last_ms(k) for k in ("block_dot2", "dcgs2_update"))
+                    if args.mode in ("dcgs2", "mgs2-lagged") else None)
     ctx.check_nan()
 
     # Krylov–Schur restart on the final factorisation (outside the timed region; reported beside

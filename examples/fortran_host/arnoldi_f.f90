@@ -43,11 +43,9 @@ program arnoldi_f
    if (nargs >= 2) then; call get_command_argument(2, arg); read (arg, *) m; end if
    st = c_null_ptr                              ! the null (default) stream
 
-   L%n_v = 512_c_int64_t*E; L%n_p = 216_c_int64_t*E; L%n_wf = 4; L%rank0 = 1    ! 3-D lx1=8, one scalar
-   L%sv = ((L%n_v + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
-   L%sp = ((L%n_p + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
-   L%ld = ((L%n_wf*L%sv + L%sp + 1 + NKV_TILE - 1)/NKV_TILE)*NKV_TILE
-   if (nkv_abi_version() /= 2) stop 'ABI mismatch'
+   if (nkv_abi_version() /= 3) stop 'ABI mismatch'
+   ! 3-D lx1=8 / lx2=6, one dotted scalar (nelt = nelv), pressure stored, this rank owns `time`
+   call ck(nkv_layout_init(L, 3, 8, 6, int(E, c_int64_t), int(E, c_int64_t), 1, 1, 1), 'layout')
 
    vbytes = int(L%ld, c_size_t)*8
    call ck(hipMalloc(Q, (m + 1)*vbytes), 'hipMalloc Q')

@@ -22,6 +22,13 @@ module nkv_bindings
       integer(c_int) function nkv_abi_version() bind(C, name="nkv_abi_version")
          import :: c_int
       end function
+      integer(c_int) function nkv_layout_init(L, ldim, lx1, lx2, nelv, nelt, n_scalars, ifpo, rank0) &
+         bind(C, name="nkv_layout_init")
+         import :: c_int, c_int64_t, nkv_layout
+         type(nkv_layout), intent(out) :: L
+         integer(c_int), value :: ldim, lx1, lx2, n_scalars, ifpo, rank0
+         integer(c_int64_t), value :: nelv, nelt
+      end function
       type(c_ptr) function nkv_last_error() bind(C, name="nkv_last_error")
          import :: c_ptr
       end function

@@ -48,7 +48,8 @@
 extern "C" {
 #endif
 
-#define NKV_ABI_VERSION 2   /* 2 (round 5): the opt-in deferred-basis DCGS2 entry points removed; rotation limited by kept columns */
+#define NKV_ABI_VERSION 3   /* 3 (round 6): nkv_layout_init added (refuses nelt != nelv); 2 (round 5): the opt-in
+                               deferred-basis DCGS2 entry points removed; rotation limited by kept columns */
 
 /* Rows per tile: fields are padded to a multiple of this many doubles. */
 #define NKV_TILE 4096
@@ -95,6 +96,16 @@ typedef struct nkv_layout {
 
 /* ---- runtime ---------------------------------------------------------- */
 int nkv_abi_version(void);
+/* Fill *L for one rank's shard from nekStab's SIZE/TOTAL facts (core/nek_vectors.f90:16-31):
+ * ldim (2/3, if3d), lx1, lx2 (pressure points per direction; ignored when !ifpo), nelv and nelt (this
+ * rank's velocity and temperature/scalar elements), n_scalars (dotted scalars: ifto + ifpsco(:)),
+ * ifpo (pressure stored), rank0 (owns the replicated `time` term).  Pads sv, sp, ld to NKV_TILE.
+ * NKV_ESHAPE when n_scalars > 0 and nelt != nelv: k_dot / real_dot dot a scalar over nelt elements
+ * with the nelv-element weights bm1s (krylov_subspace.f90:36-44, nek_vectors.f90:88-99, NEKSTAB:86),
+ * i.e. past the end of bm1s, so conjugate heat transfer layouts have no reference result and are
+ * refused.  NKV_EINVAL on bad parameters. */
+int nkv_layout_init(nkv_layout* L, int ldim, int lx1, int lx2, int64_t nelv, int64_t nelt, int n_scalars,
+                    int ifpo, int rank0);
 const char* nkv_last_error(void);
 /* Device properties of the current HIP device (host sync-free). */
 int nkv_device_info(int* device, int* cu_count, int64_t* hbm_bytes, char* name, int name_len);

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see module d
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnekkrylov.so")
 
-NKV_ABI_VERSION = 2
+NKV_ABI_VERSION = 3
 NKV_TILE = 4096
 NKV_MAX_COLS = 1024   # most columns per multi-dot (include/nekkrylov.h)
 NKV_ROT_MAX_OUT = 256   # most output columns of a basis rotation with more than 16 kept (include/nekkrylov.h)
@@ -71,6 +71,7 @@ ALLREDUCE_FN = CFUNCTYPE(c_int, c_void_p, c_void_p, c_int, c_void_p)
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "nkv_abi_version": (c_int, []),
+    "nkv_layout_init": (c_int, [_L, c_int, c_int, c_int, c_int64, c_int64, c_int, c_int, c_int]),
     "nkv_last_error": (c_char_p, []),
     "nkv_device_info": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int64), c_char_p, c_int]),
     "nkv_workspace_bytes": (c_size_t, [_L, c_int]),

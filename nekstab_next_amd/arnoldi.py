@@ -578,12 +578,18 @@ class FactorizationGraph:
         self.ctx, self.op, self.Q, self.Hd, self.f, self.mode = ctx, op, Q, Hd, f, mode
         self.graphs = {}
 
+    # modes that synchronise with the host inside every step (the lagged MGS coefficients are solved
+    # on the host from a downloaded multi-dot; the native twin synchronises its stream per step): a
+    # graph capture of them fails, so they always launch eagerly
+    HOST_SYNC_MODES = ("mgs2-lagged", "mgs2-lagged-native")
+
     def usable(self) -> bool:
-        """Single rank only.  Capturing RCCL all-reduces into a replayed graph has never run on more
-        than one GPU (round 1 rehearsed world > 1 only as gloo ranks sharing one GPU), so a
-        multi-rank factorisation always launches eagerly; ``krylov_schur`` refuses
-        ``graphs=True`` at world > 1 instead of silently falling back."""
-        return self.ctx.comm.world == 1
+        """Single rank and a capturable mode only.  Capturing RCCL all-reduces into a replayed graph
+        has never run on more than one GPU (round 1 rehearsed world > 1 only as gloo ranks sharing
+        one GPU), so a multi-rank factorisation always launches eagerly; ``krylov_schur`` refuses
+        ``graphs=True`` at world > 1 instead of silently falling back.  The host-synchronising
+        lagged modes (``HOST_SYNC_MODES``) launch eagerly at any world size."""
+        return self.ctx.comm.world == 1 and self.mode not in self.HOST_SYNC_MODES
 
     def run(self, mstart: int, mend: int, transpose: bool = False) -> None:
         if mend < mstart:

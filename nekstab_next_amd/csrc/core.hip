@@ -52,6 +52,35 @@ extern "C" {
 
 int nkv_abi_version(void) { return NKV_ABI_VERSION; }
 
+int nkv_layout_init(nkv_layout* L, int ldim, int lx1, int lx2, int64_t nelv, int64_t nelt, int n_scalars,
+                    int ifpo, int rank0) {
+    if (!L) return fail(NKV_EINVAL, "layout is NULL");
+    if ((ldim != 2 && ldim != 3) || lx1 < 2 || (ifpo && lx2 < 1) || nelv < 0 || n_scalars < 0)
+        return fail(NKV_EINVAL, "bad layout parameters: ldim=%d lx1=%d lx2=%d nelv=%lld n_scalars=%d", ldim, lx1,
+                    lx2, (long long)nelv, n_scalars);
+    // k_dot / real_dot weight a scalar over nt = nx1*ny1*nz1*nelt points with bm1s(lx1,ly1,lz1,lelv)
+    // (core/krylov_subspace.f90:36-44, nek_vectors.f90:88-99, core/NEKSTAB:86): with nelt != nelv
+    // (conjugate heat transfer) the reference reads past its weights, so such a layout is refused
+    if (n_scalars > 0 && nelt != nelv)
+        return fail(NKV_ESHAPE, "nelt=%lld != nelv=%lld with %d dotted scalar(s): conjugate heat transfer "
+                    "layouts are not supported (the reference weights t over nelt elements with the nelv-element "
+                    "bm1s, krylov_subspace.f90:36-44, NEKSTAB:86)", (long long)nelt, (long long)nelv, n_scalars);
+    int64_t pv = lx1, pp = ifpo ? lx2 : 0;
+    for (int d = 1; d < ldim; ++d) {
+        pv *= lx1;
+        pp *= ifpo ? lx2 : 0;
+    }
+    auto up = [](int64_t n) { return (n + NKV_TILE - 1) / NKV_TILE * NKV_TILE; };
+    L->n_v = pv * nelv;
+    L->n_p = pp * nelv;
+    L->sv = up(L->n_v);
+    L->sp = up(L->n_p);
+    L->n_wf = ldim + n_scalars;
+    L->ld = up((int64_t)L->n_wf * L->sv + L->sp + 1);
+    L->rank0 = rank0 ? 1 : 0;
+    return NKV_OK;
+}
+
 const char* nkv_last_error(void) { return g_err; }
 
 int nkv_device_info(int* device, int* cu_count, int64_t* hbm_bytes, char* name, int name_len) {

@@ -30,6 +30,9 @@ class NekLayout:
     n_scalars : active scalar fields in the dot (``ifto`` + ``ifpsco(:)``), 0 for pure flow
     ifpo      : pressure stored (``ifpo``); when False the pressure segment is empty
     rank/world: this shard of an element-contiguous partition
+    nelgt     : global number of temperature/scalar elements (Nek5000's ``nelgt``), None = nelgv.
+                Only ``nelgt == nelgv`` is supported when a scalar is dotted: conjugate heat
+                transfer (``nelt > nelv``) is refused, see ``__post_init__``.
     """
 
     ldim: int
@@ -40,6 +43,7 @@ class NekLayout:
     ifpo: bool = True
     rank: int = 0
     world: int = 1
+    nelgt: int | None = None
 
     def __post_init__(self):
         if self.ldim not in (2, 3):
@@ -48,6 +52,16 @@ class NekLayout:
             raise ValueError("bad layout parameters")
         if not (0 <= self.rank < self.world):
             raise ValueError("rank out of range")
+        if self.nelgt is not None and self.nelgt != self.nelgv and self.n_scalars > 0:
+            # the reference dots a scalar over nt = nx1*ny1*nz1*nelt points with the velocity-mesh
+            # weights bm1s(lx1,ly1,lz1,lelv) (core/krylov_subspace.f90:36-44, nek_vectors.f90:88-99;
+            # bm1s declared at core/NEKSTAB:86): with nelt > nelv it reads past bm1s, so there is no
+            # reference result to reproduce.  Every weighted field here has n_v points and shares one
+            # weight array; such a layout is refused rather than given a made-up meaning.
+            raise ValueError(f"nelgt={self.nelgt} != nelgv={self.nelgv} with {self.n_scalars} dotted scalar(s): "
+                             "conjugate heat transfer layouts (nelt > nelv) are not supported — the reference "
+                             "weights the scalar over nelt elements with the nelv-element bm1s "
+                             "(krylov_subspace.f90:36-44, NEKSTAB:86)")
 
     # ---- per element ------------------------------------------------------------------------
     @property
@@ -69,7 +83,8 @@ class NekLayout:
         return (r * self.nelgv) // self.world, ((r + 1) * self.nelgv) // self.world
 
     def shard(self, rank: int, world: int) -> "NekLayout":
-        return NekLayout(self.ldim, self.lx1, self.lx2, self.nelgv, self.n_scalars, self.ifpo, rank, world)
+        return NekLayout(self.ldim, self.lx1, self.lx2, self.nelgv, self.n_scalars, self.ifpo, rank, world,
+                         self.nelgt)
 
     @property
     def nelv(self) -> int:

@@ -30,3 +30,16 @@ def test_survey_model_matches_worked_total():
     N, N_w, n_v, m = 100_014_464, 90_472_448, 22_618_112, 128
     tot = bench.survey_model_bytes(N, N_w, n_v, m) - m * 8.0 * 3 * N
     assert abs(tot / 1e12 - 26.03) < 0.01
+
+
+def test_lagged_mode_byte_model():
+    """``bench.py --mode mgs2-lagged`` has a byte model — the DCGS2 kernels' bytes (the
+    same two-vector dot and dual update per step) plus the weights of its closing fused norm — and
+    its native twin moves the same bytes."""
+    import bench
+
+    N, N_w, n_v, m = 100_014_464, 90_472_448, 22_618_112, 128
+    d = bench.executed_bytes(N, N_w, n_v, m, "dcgs2")
+    lg = bench.executed_bytes(N, N_w, n_v, m, "mgs2-lagged")
+    assert lg == d + 8.0 * n_v
+    assert bench.executed_bytes(N, N_w, n_v, m, "mgs2-lagged-native") == lg

@@ -237,3 +237,20 @@ def test_segment_entry_points_are_noops_on_an_empty_shard():
     full = velocity_layout(cylinder_layout(2))
     assert lib.nkv_wavemaker(ctypes.byref(full.c_struct()), None, None, None, None, None, 2, None) != 0
     assert "NULL" in _lib.last_error()
+
+
+def test_graph_replay_refused_for_host_synchronising_modes():
+    """the lagged MGS modes synchronise with the host every step, so a HIP-graph capture
+    of their factorisation would fail; FactorizationGraph.usable() refuses them (krylov_schur then
+    launches eagerly), and still refuses every mode at world size > 1."""
+    from types import SimpleNamespace
+
+    from nekstab_next_amd.arnoldi import FactorizationGraph
+
+    def fg(mode, world=1):
+        return FactorizationGraph(SimpleNamespace(comm=SimpleNamespace(world=world)), None, None, None, None, mode)
+
+    for mode in ("mgs2-lagged", "mgs2-lagged-native"):
+        assert not fg(mode).usable()
+    for mode in ("dcgs2", "cgs2", "mgs2", "mgs2-icwy", "dcgs2-native"):
+        assert fg(mode).usable() and not fg(mode, world=2).usable()

@@ -93,7 +93,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(_lib.EXPORTED) == syms  # the ctypes table types every declared entry point
-    assert lib.nkv_abi_version() == _lib.NKV_ABI_VERSION == 2
+    assert lib.nkv_abi_version() == _lib.NKV_ABI_VERSION == 3
 
 
 def test_header_constants_match_python():
@@ -155,3 +155,35 @@ def test_fortran_host_example_builds():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert os.path.exists(os.path.join(root, "examples", "fortran_host", "arnoldi_f"))
+
+
+def test_layout_init_matches_neklayout_and_refuses_cht():
+    """nkv_layout_init (ABI 3) pads a shard exactly as NekLayout.c_struct does, on the host (no GPU
+    call), and refuses nelt != nelv with a dotted scalar: the reference weights
+    the scalar over nelt elements with the nelv-element bm1s (krylov_subspace.f90:36-44,
+    NEKSTAB:86), so conjugate heat transfer has no reference result.  NekLayout refuses it too."""
+    import ctypes
+
+    from nekstab_next_amd import _lib
+    from nekstab_next_amd.layout import NekLayout
+
+    lib = _lib.load()
+    for ldim, lx1, lx2, E, ns, ifpo in ((3, 8, 6, 44176, 1, True), (2, 6, 4, 1996, 0, True), (3, 5, 3, 17, 2, True),
+                                        (2, 6, 4, 100, 1, False), (3, 8, 6, 0, 1, True)):
+        lay = NekLayout(ldim, lx1, lx2, E, ns, ifpo)
+        want = lay.c_struct()
+        got = _lib.nkv_layout()
+        rc = lib.nkv_layout_init(ctypes.byref(got), ldim, lx1, lx2, lay.nelv, lay.nelv, ns, int(ifpo), 1)
+        assert rc == _lib.NKV_OK, _lib.last_error()
+        for k in ("n_v", "n_p", "sv", "sp", "ld", "n_wf", "rank0"):
+            assert getattr(got, k) == getattr(want, k), (k, ldim, lx1, E)
+    bad = _lib.nkv_layout()
+    assert lib.nkv_layout_init(ctypes.byref(bad), 3, 8, 6, 100, 120, 1, 1, 1) == _lib.NKV_ESHAPE
+    assert "conjugate heat transfer" in _lib.last_error()
+    # without a dotted scalar the temperature mesh is irrelevant to the dot
+    assert lib.nkv_layout_init(ctypes.byref(bad), 3, 8, 6, 100, 120, 0, 1, 1) == _lib.NKV_OK
+    assert lib.nkv_layout_init(ctypes.byref(bad), 4, 8, 6, 100, 100, 0, 1, 1) == _lib.NKV_EINVAL
+    with pytest.raises(ValueError, match="conjugate heat transfer"):
+        NekLayout(3, 8, 6, 100, 1, nelgt=120)
+    NekLayout(3, 8, 6, 100, 0, nelgt=120)   # no dotted scalar: accepted
+    assert NekLayout(3, 8, 6, 100, 1, nelgt=100).shard(1, 2).nelgt == 100
