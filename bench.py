@@ -311,11 +311,15 @@ PORT_NOTE = ("the C port runs up to ~1.7x slower than the reference's own Fortra
 def host_baselines(args, m: int, gpu_ms: float) -> dict:
     """The three CPU lines timed live on this host (rank 0 only, after every rank has left the
     process group at world > 1, so no peer waits in a collective meanwhile), each led by its
-    measured full-size figures where they exist."""
+    measured full-size figures where they exist.  The all-threads sample shrinks with the thread
+    count (E = cpu_E x threads / 16, at least cpu_E_1core) so that it stays a bounded ~30 s of CPU
+    work when a launcher leaves few threads (torch.distributed.run sets OMP_NUM_THREADS=1 unless
+    the environment sets it)."""
     host = host_threads()
-    cpu = cpu_baseline(args.cpu_E, m, host["threads"])
+    e_all = max(args.cpu_E_1core, min(args.cpu_E, args.cpu_E * host["threads"] // 16))
+    cpu = cpu_baseline(e_all, m, host["threads"])
     cpu1 = cpu_baseline(args.cpu_E_1core, m, 1)
-    cpu_opt = cpu_baseline(args.cpu_E, m, host["threads"], variant="cgs2")
+    cpu_opt = cpu_baseline(e_all, m, host["threads"], variant="cgs2")
     lead_with_measured(cpu, cpu_full_size_run(args.E, m, gpu_ms, "mgs2", host["threads"]), gpu_ms)
     lead_with_measured(cpu1, cpu_full_size_run(args.E, m, gpu_ms, "mgs2", 1), gpu_ms)
     lead_with_measured(cpu_opt, cpu_full_size_run(args.E, m, gpu_ms, "cgs2", host["threads"]), gpu_ms)
@@ -717,6 +721,22 @@ def run(args):
         ks_restart = krylov_schur_leg(ctx, lay, Q, d_cl, exact_cl, seed, m, 4, warmup=False,
                                       operator="clustered: 1 - 0.002 (k - 1/2), k <= 400, over U[0, 0.2]")
         del d_cl
+        if restart is not None and ks_restart["mstart_history"]:
+            # the restart leg's own kept-column count (25 of 128 at BASELINE size: the 17-64-kept MFMA
+            # rotation), repeated on the random orthogonal V for its steady rate
+            n_w = int(ks_restart["mstart_history"][0]) - 1
+            rw = PhaseTimer(dev)
+            ctx.timer = rw
+            for _ in range(3):
+                rw.begin("rotate_wide")
+                ctx.call("nkv_rotate_cols", Q.ptr, m, V.data_ptr(), m, n_w, ctx.stream)
+                rw.end("rotate_wide", 8.0 * lay.N * (m + n_w))
+            ctx.timer = None
+            wp = rw.summary()["rotate_wide"]
+            restart.update({"rotate_wide_kept": n_w, "rotate_wide_ms": round(wp["avg_ms"], 3),
+                            "rotate_wide_gbs": round(wp["gbps"], 1),
+                            "rotate_wide_frac_hbm": round(wp["gbps"] / HBM_PEAK_GBS, 4),
+                            "rotate_wide_tflops": round(2.0 * lay.N * m * n_w / (wp["avg_ms"] * 1e-3) / 1e12, 2)})
     else:
         del d_scaled
 

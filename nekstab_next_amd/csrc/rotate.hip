@@ -141,6 +141,136 @@ __global__ __launch_bounds__(WAVES * 64) void k_rotate_stream(double* __restrict
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Restart rotation, wide-load streaming form (17 .. 16*NKV_ROTW_MAX_MB kept columns, V in LDS whole):
+// as k_rotate_stream, but every lane loads 16 B (rows 2r, 2r+1 of one column), so a wave
+// instruction reads 4 columns x 256 contiguous bytes and feeds TWO MFMAs per V operand (the even
+// and the odd rows of a 32-row slab: two 16x16 output tiles).  The k-rows past k are clamped to
+// column k-1 (V is zero there in LDS), so no load carries a per-lane guard and the compiler can
+// wait for exactly the batch an MFMA group consumes (a guarded load is an exec-masked branch, after
+// which it waits for every load in flight).  Three batches rotate through registers, two ahead of
+// the MFMAs; the next tile's first two batches are issued before this tile's stores.  V sits in
+// LDS k-major, Vs[i * cp + c] with cp = 16 (mod 32) doubles: the 16 lanes of one k-row read 128
+// contiguous bytes and the next k-row lands on the other half of the banks (no conflicts for
+// ds_read_b64, nor for the ds_read2_b64 the compiler forms from two column blocks).
+// In place is safe as in k_rotate_stream: a wave consumes all k inputs of its 32 rows before it
+// stores any of their n_out outputs, and no other wave touches those rows.
+// ------------------------------------------------------------------------------------------
+template <int MB, int WAVES, int U>
+__global__ __launch_bounds__(WAVES * 64) void k_rotate_wide(double* __restrict__ Q, int64_t ld, int k,
+                                                            const double* __restrict__ V, int ldv, int n_out,
+                                                            int cp, int64_t t_lo, int64_t t_hi) {
+    extern __shared__ __attribute__((aligned(16))) double Vs[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int nb = (k + 4 * U - 1) / (4 * U);   // batches of U k-steps of 4
+    const int kpad = nb * 4 * U;
+    // Vs[i][c] for i < kpad, c < cp (zero beyond k / n_out); V is read column by column (coalesced)
+    for (int e = threadIdx.x; e < kpad * 16 * MB; e += WAVES * 64) {
+        const int c = e / kpad, i = e % kpad;
+        Vs[i * cp + c] = (i < k && c < n_out) ? V[i + (int64_t)c * ldv] : 0.0;
+    }
+    __syncthreads();
+    const double* vs = Vs + lk * cp + lr;
+    const int kl = k - 1, nf = k / (4 * U);   // nf: batches whose k-rows are all < k
+    // a lane's byte offset from its wave's (uniform) row base: SGPR base + 32-bit VGPR offset per
+    // load, with no per-lane 64-bit address arithmetic (lk * ld * 8 < 4 GB: ld < 2^27 doubles)
+    const uint32_t lane_off = (uint32_t)(((int64_t)lk * ld + 2 * lr) * (int64_t)sizeof(double));
+    typedef double2 Batch[U];
+    int64_t tile = t_lo + blockIdx.x;   // this launch's row band: tiles [t_lo, t_hi)
+    if (tile >= t_hi) return;
+    auto wbase = [&](int64_t t) { return Q + (t * WAVES + wave) * 32; };
+    const double* qw = wbase(tile);
+    auto load_full = [&](Batch& b, const double* qq, int t) {   // batch t < nf
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = ldq(at_b(qq + (int64_t)(t * 4 * U + 4 * u) * ld, lane_off));
+    };
+    auto load = [&](Batch& b, const double* qq, int t) {   // any batch t < nb: the k-rows past k are clamped
+        if (t < nf) {
+            load_full(b, qq, t);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = t * 4 * U + 4 * u + lk;
+                b[u] = ldq(qq + (int64_t)(i < kl ? i : kl) * ld + 2 * lr);
+            }
+        }
+    };
+    nkv_f64x4 acc[2][MB];
+    auto mma = [&](const Batch& b, int t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                const double a = vs[(t * 4 * U + 4 * u) * cp + m * 16];
+                acc[0][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u].x, acc[0][m], 0, 0, 0);
+                acc[1][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[u].y, acc[1][m], 0, 0, 0);
+            }
+        }
+    };
+    // the issue order is the pipeline: keep the scheduler from moving loads across MFMA groups
+#define NKV_ROTW_FENCE __builtin_amdgcn_sched_barrier(0)
+    // prologue and next-tile loads are unconditional (batch 1 of a one-batch k is clamped, the tile
+    // after the last one re-reads the last): every path into the loop has the same loads in flight,
+    // so the compiler's wait counts stay exact
+    Batch b0, b1, b2;
+    load(b0, qw, 0);
+    load(b1, qw, 1);
+    for (;;) {
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            acc[0][m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
+            acc[1][m] = nkv_f64x4{0.0, 0.0, 0.0, 0.0};
+        }
+        int t = 0;
+        // steady trips: the three batches loaded here (t+2, t+3, t+4) are whole: no branch between a
+        // load and the MFMAs that wait for it
+        for (; t + 4 < nf; t += 3) {
+            NKV_ROTW_FENCE;
+            load_full(b2, qw, t + 2);
+            NKV_ROTW_FENCE;
+            mma(b0, t);
+            NKV_ROTW_FENCE;
+            load_full(b0, qw, t + 3);
+            NKV_ROTW_FENCE;
+            mma(b1, t + 1);
+            NKV_ROTW_FENCE;
+            load_full(b1, qw, t + 4);
+            NKV_ROTW_FENCE;
+            mma(b2, t + 2);
+        }
+        NKV_ROTW_FENCE;
+        // b0 holds batch t < nb, b1 batch t+1 when it exists: the rest (wave-uniform branches)
+        for (;; t += 2) {
+            mma(b0, t);
+            if (t + 1 >= nb) break;
+            const bool more2 = t + 2 < nb;
+            if (more2) load(b0, qw, t + 2);
+            mma(b1, t + 1);
+            if (!more2) break;
+            if (t + 3 < nb) load(b1, qw, t + 3);
+        }
+        NKV_ROTW_FENCE;
+#undef NKV_ROTW_FENCE
+        // the next tile's first two batches go out before this tile's stores (other rows)
+        const int64_t next = tile + gridDim.x;
+        double* qo = const_cast<double*>(qw) + 2 * lr;
+        qw = wbase(next < t_hi ? next : tile);
+        load(b0, qw, 0);
+        load(b1, qw, 1);
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gc = m * 16 + lk + 4 * r;
+                if (gc < n_out) st2s(qo + (int64_t)gc * ld, make_double2(acc[0][m][r], acc[1][m][r]));
+            }
+        }
+        if (next >= t_hi) break;
+        tile = next;
+    }
+}
+
 #ifndef NKV_ROT_CHUNK_SB
 #define NKV_ROT_CHUNK_SB 1
 #endif
@@ -334,8 +464,10 @@ static_assert(NKV_TILE % (4 * 16) == 0 && NKV_TILE % (8 * 16) == 0, "a 16-row sl
 template <int MB>
 int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out,
                                 int kp, size_t lds, void* stream) {
-    // register budget: ~21*MB + 55 VGPRs (U = 8); 16 waves/WG allow 128 per lane, so wide column blocks
-    // run with half the waves (256 VGPRs)
+    // register budget (gfx950, U = 4, measured with -Rpass-analysis=kernel-resource-usage in round 6):
+    // MB = 1/2/3 at 16 waves per workgroup 52/74/96 VGPRs; MB = 4..8 at 8 waves 118/146/168/235/245 (the
+    // three-batch path from MB = 5), no spills; 16 waves/WG allow 128 per lane, so wide column blocks run
+    // with half the waves (256 VGPRs)
     constexpr int NB = NKV_ROT_NB, W = MB <= 3 ? NKV_ROT_WAVES : NKV_ROT_WAVES / 2, U = NKV_ROT_U;
     auto kern = k_rotate_stream<NB, MB, W, U>;
     static bool attr_set = false;
@@ -353,6 +485,60 @@ int launch_rotate_stream(const nkv_layout* L, double* Q, int k, const double* V,
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(W * 64), lds, S(stream), Q, L->ld, k, V, ldv, n_out, kp,
                        n_tiles);
     NKV_LAUNCHED();
+    return NKV_OK;
+}
+
+#ifndef NKV_ROTW
+#define NKV_ROTW 1   // 0: never use the wide-load rotation (the k_rotate_stream / k_rotate_chunked path)
+#endif
+#ifndef NKV_ROTW_MAX_MB
+#define NKV_ROTW_MAX_MB 4   // wide-load rotation up to this many 16-column blocks (64 kept columns)
+#endif
+#ifndef NKV_ROTW_W
+#define NKV_ROTW_W 8   // waves per workgroup of the wide-load rotation
+#endif
+#ifndef NKV_ROTW_U
+#define NKV_ROTW_U 4   // k-steps of 4 per batch of the wide-load rotation
+#endif
+#ifndef NKV_ROTW_ROUNDS
+#define NKV_ROTW_ROUNDS 0   // wide-load rotation: one launch per this many grid-stride rounds (0: one launch; bands
+                            // lose here: 2 rounds -10 %, 8 rounds -2 %, profiles/r06d_tune_rotw_bands.log)
+#endif
+static_assert(NKV_TILE % (NKV_ROTW_W * 32) == 0, "a 32-row slab per wave must tile the padding");
+
+// LDS of the wide-load rotation: V k-major, kpad rows of cp doubles (cp = 16 mod 32)
+inline int rotw_cp(int nact) { return ((16 * nact + 31) / 32) * 32 + 16; }
+inline int rotw_kpad(int k) { return ((k + 4 * NKV_ROTW_U - 1) / (4 * NKV_ROTW_U)) * 4 * NKV_ROTW_U; }
+
+template <int MB>
+int launch_rotate_wide(const nkv_layout* L, double* Q, int k, const double* V, int ldv, int n_out, void* stream) {
+    constexpr int W = NKV_ROTW_W, U = NKV_ROTW_U;
+    auto kern = k_rotate_wide<MB, W, U>;
+    const int cp = rotw_cp(MB);
+    const size_t lds = (size_t)rotw_kpad(k) * cp * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        NKV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    const int64_t n_tiles = rows_of(L) / ((int64_t)W * 32);
+    if (n_tiles < 1) return NKV_OK;
+    // persistent grid: as many workgroups as are resident at once (registers, LDS and waves per CU)
+    int per_cu = 0;
+    NKV_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, W * 64, lds));
+    if (per_cu < 1) per_cu = 1;
+    const int64_t g0 = (int64_t)device_cus() * per_cu;
+    const int64_t g = n_tiles < g0 ? n_tiles : g0;
+    // one launch per row band of NKV_ROTW_ROUNDS grid-stride rounds, as the few-column rotation and
+    // the DCGS2 updates: the workgroups stay on one compact window of rows, reading each column in
+    // step, instead of drifting apart over the whole vector (0: one persistent launch)
+    const int64_t band = NKV_ROTW_ROUNDS > 0 ? (int64_t)NKV_ROTW_ROUNDS * g : n_tiles;
+    for (int64_t lo = 0; lo < n_tiles; lo += band) {
+        const int64_t hi = lo + band < n_tiles ? lo + band : n_tiles;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(g < hi - lo ? g : hi - lo)), dim3(W * 64), lds, S(stream), Q, L->ld,
+                           k, V, ldv, n_out, cp, lo, hi);
+        NKV_LAUNCHED();
+    }
     return NKV_OK;
 }
 
@@ -435,6 +621,24 @@ int nkv_rotate_cols(const nkv_layout* L, double* Q, int k, const double* V_dev, 
             case 15: return launch_rotate_few<15>(L, Q, k, V_dev, ldv, stream);
             case 16: return launch_rotate_few<16>(L, Q, k, V_dev, ldv, stream);
             default: break;
+        }
+    }
+    if (NKV_ROTW && (n_out + 15) / 16 <= NKV_ROTW_MAX_MB && rows_of(L) % ((int64_t)NKV_ROTW_W * 32) == 0) {
+        const int nact = (n_out + 15) / 16;
+        if ((size_t)rotw_kpad(k) * rotw_cp(nact) * sizeof(double) <= 160 * 1024) {
+            switch (nact) {
+                case 1: return launch_rotate_wide<1>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 2: return launch_rotate_wide<2>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 3: return launch_rotate_wide<3>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 4: return launch_rotate_wide<4>(L, Q, k, V_dev, ldv, n_out, stream);
+#if NKV_ROTW_MAX_MB > 4
+                case 5: return launch_rotate_wide<5>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 6: return launch_rotate_wide<6>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 7: return launch_rotate_wide<7>(L, Q, k, V_dev, ldv, n_out, stream);
+                case 8: return launch_rotate_wide<8>(L, Q, k, V_dev, ldv, n_out, stream);
+#endif
+                default: break;
+            }
         }
     }
     if (NKV_ROT_STREAM && (n_out + 15) / 16 < NKV_ROT_CHUNK_FROM &&

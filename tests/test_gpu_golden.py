@@ -56,7 +56,7 @@ def _first_factorisation(ctx, op, seed, k, mode):
     return Hd.download()
 
 
-@pytest.mark.parametrize("mode", ["dcgs2", "dcgs2-native", "cgs2", "mgs2"])
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2", "mgs2"])
 def test_golden_config1(gpu, mode):
     lay = NekLayout(ldim=2, lx1=6, lx2=4, nelgv=1136)
     z = _load("ks_config1.npz")
@@ -130,7 +130,7 @@ def test_golden_restart_m128(gpu, mode):
         assert np.min(np.abs(exact - v)) <= 1e-10
 
 
-@pytest.mark.parametrize("mode", ["dcgs2", "dcgs2-native", "cgs2"])
+@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
 def test_golden_config3_k32(gpu, mode):
     """Config 3's operator family at E=128 (N=289,792), Krylov–Schur k_dim=32, schur_tgt=4: the MKL
     trajectory (10 converged in the first factorisation) and Ritz values 1e-10; top 4 = exact."""

@@ -209,7 +209,14 @@ def test_rotate_vs_oracle(gpu, k):
 
 @pytest.mark.parametrize("k,n_out", [(7, 3), (100, 1), (128, 6), (128, 8), (9, 9), (4, 4), (131, 5), (576, 7),
                                      (128, 12), (130, 13), (64, 16), (1000, 11), (128, 20), (129, 17), (256, 255),
-                                     (300, 150), (576, 33), (900, 6), (256, 100), (200, 128), (576, 256)])
+                                     (300, 150), (576, 33), (900, 6), (256, 100), (200, 128), (576, 256),
+                                     # k_rotate_wide (17-64 kept, V in LDS): every column-block count, whole
+                                     # and partial last batches (k % 16), one-batch k, k = n_out
+                                     (128, 25), (100, 17), (130, 48), (64, 64), (129, 33), (37, 33), (17, 17),
+                                     (200, 40), (18, 18), (250, 64),
+                                     # k_rotate_stream two batches ahead (65-128 kept): MB 5..8, zero
+                                     # and several steady trips, every tail branch
+                                     (83, 70), (128, 65), (96, 96), (128, 128), (150, 100)])
 def test_rotate_cols_vs_oracle(gpu, k, n_out):
     """Partial restart rotation: Q[:, :n_out] = Q[:, :k] V[:, :n_out]; columns n_out..k untouched."""
     lay = LAYOUTS["2d"]
@@ -427,7 +434,7 @@ def test_native_breakdown_flag_and_mgs2_fallback(gpu, rank):
     np.testing.assert_array_equal(res[0][1], res[1][1])
 
 
-@pytest.mark.parametrize("mode", ["cgs2", "cgs2-native", "mgs2", "dcgs2"])
+@pytest.mark.parametrize("mode", ["cgs2", "mgs2", "dcgs2"])
 @pytest.mark.parametrize("name", list(LAYOUTS))
 def test_arnoldi_hessenberg_vs_oracle(gpu, mode, name):
     lay = LAYOUTS[name]

@@ -17,7 +17,9 @@ INTERNAL = os.path.join(CSRC, "nkv_internal.h")
 REMOVED = ["NKV_DC_EXPERIMENT", "NKV_DC_SYNC", "NKV_QTILE_EXP", "NKV_D2_FIELDMAJOR", "NKV_DC_SCHED",
            "NKV_D2_SCHED", "NKV_ST_AUX", "NKV_XCD_MAP", "NKV_DC_FIELDLOOP", "NKV_FUSE_PF", "NKV_LD_ALIGN"]
 RETIRED = ["k_rotate_mfma", "k_dcgs2_lazy_update", "NKV_ROT_VALU", "NKV_ROT_SMALLR", "NKV_ROT_CHUNKED", "NKV_DL_U",
-           "dcgs2_coef_lazy", "dcgs2_update_lazy", "NKV_ROT_MAX_K"]
+           "dcgs2_coef_lazy", "dcgs2_update_lazy", "NKV_ROT_MAX_K",
+           # round 6: the LDS-staged rotation and the wide kernel's timing diagnostics (experiment patches)
+           "k_rotate_glds", "NKV_ROTG", "NKV_ROTW_DIAG", "NKV_ROTW_APRE"]
 
 
 def _sources():
@@ -73,9 +75,11 @@ def test_no_kernel_copy_in_tools():
     text = "".join(open(p).read() for p in _sources())
     for name, v in tk.VARIANTS.items():
         assert "src" not in v, name
+        # a knob lives in the product sources, or in the experiment patch that adds it
+        t = text + (open(os.path.join(exp, v["patch"] + ".patch")).read() if "patch" in v else "")
         for knob in v:
             if knob != "patch":
-                assert re.search(r"#ifndef %s\b" % knob, text), (name, knob)
+                assert re.search(r"#ifndef %s\b" % knob, t), (name, knob)
 
 
 def test_experiment_patches_apply(tmp_path):

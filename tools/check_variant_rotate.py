@@ -4,7 +4,7 @@ same inputs: nkv_rotate_cols over a hashed basis for several (k, n_out).  Used b
 schedule change of a rotation kernel moves from the experiment copy into the product (the MFMA
 accumulation order must not change, so the results must be identical bit for bit).
 
-usage (on the MI355X box): python tools/check_variant_rotate.py BASE_VARIANT NEW_VARIANT
+usage (on the MI355X box): python tools/check_variant_rotate.py BASE_VARIANT NEW_VARIANT [--report-only]
 """
 import ctypes
 import os
@@ -25,6 +25,8 @@ def main():
     for n in sys.argv[1:3]:
         L = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"lib_{n}.so"))
         for name, (res, args) in _lib._SIGNATURES.items():
+            if not hasattr(L, name):   # a build older than the current ABI
+                continue
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
         libs.append(L)
@@ -34,8 +36,9 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     dev = torch.device("cuda", 0)
     bad = 0
-    for k, n_out in ((128, 128), (128, 20), (128, 64), (37, 33), (200, 17), (96, 96), (150, 40),
-                     (200, 100), (200, 200), (257, 129), (1000, 40)):
+    for k, n_out in ((128, 128), (128, 20), (128, 25), (128, 64), (37, 33), (200, 17), (96, 96), (150, 40),
+                     (200, 100), (200, 200), (257, 129), (1000, 40), (100, 17), (130, 48), (64, 64), (17, 17),
+                     (129, 33), (83, 70), (128, 65), (150, 100)):
         outs = []
         V = torch.as_tensor(np.random.default_rng(k * 1000 + n_out).standard_normal((n_out, k))).to(dev)
         for L in libs:
@@ -49,7 +52,7 @@ def main():
         diff = float(np.max(np.abs(outs[0] - outs[1])))
         print(f"k={k:4d} n_out={n_out:4d} bit-identical={same} max|diff|={diff:.3e}", flush=True)
         bad += 0 if same else 1
-    sys.exit(1 if bad else 0)
+    sys.exit(1 if bad and "--report-only" not in sys.argv else 0)
 
 
 if __name__ == "__main__":

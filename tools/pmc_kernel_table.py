@@ -36,13 +36,17 @@ def table(pass_root):
     per = collections.defaultdict(lambda: collections.defaultdict(list))   # kernel -> counter -> [per dispatch]
     for f in sorted(glob.glob(os.path.join(pass_root, "p*", "**", "*counter_collection.csv"), recursive=True)):
         val = collections.defaultdict(float)
-        kname = {}
+        kname, dur = {}, {}
         for r in csv.DictReader(open(f)):
             d = int(r["Dispatch_Id"])
             kname[d] = short(r["Kernel_Name"])
             val[(d, r["Counter_Name"])] += float(r["Counter_Value"])
+            if "End_Timestamp" in r and r["End_Timestamp"]:
+                dur[d] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         for (d, c), v in val.items():
             per[kname[d]][c].append(v)
+        for d, t in dur.items():
+            per[kname[d]]["duration_ns"].append(t)
     out = {}
     for k, cs in per.items():
         if not k.startswith("k_"):
@@ -52,6 +56,10 @@ def table(pass_root):
         cyc = b.get("GRBM_GUI_ACTIVE")
         if cyc:
             b["gui_cycles_per_xcd"] = cyc / N_XCD
+            if b.get("duration_ns"):   # the clock the chip held (MI355X_MICROARCH.md 'DVFS give-back')
+                b["effective_clock_ghz"] = cyc / N_XCD / b["duration_ns"]
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in b:   # per SIMD (1024 of them)
+                b["mfma_busy_frac"] = b["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc / N_XCD * 4 * N_CU)
         wc = b.get("SQ_WAVE_CYCLES")
         if wc:
             for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
@@ -87,7 +95,8 @@ def table(pass_root):
 def main():
     out = table(sys.argv[1])
     json.dump(out, open(sys.argv[2], "w"), indent=1, sort_keys=True)
-    keys = ("dispatches", "gui_cycles_per_xcd", "SQ_WAIT_INST_ANY/wave_cycle", "SQ_ACTIVE_INST_VMEM/wave_cycle",
+    keys = ("dispatches", "duration_ns", "effective_clock_ghz", "mfma_busy_frac", "gui_cycles_per_xcd",
+            "SQ_WAIT_INST_ANY/wave_cycle", "SQ_ACTIVE_INST_VMEM/wave_cycle",
             "vmem_in_flight_per_wave", "L2_read_latency_cycles", "mfma_f64_per_cycle_per_cu", "hbm_read_bytes",
             "hbm_write_bytes")
     for k, b in sorted(out.items()):

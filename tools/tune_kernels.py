@@ -151,6 +151,37 @@ VARIANTS = {
     # has the same guarded loads: the steady chunks with unguarded ones are bit-identical but
     # 12-55 % slower at k = 160-200 (r05al): not adopted
     "rot_chunk_unc": {"patch": "rot_chunk_unc"},
+    # round 6: the wide-load rotation (k_rotate_wide: 16 B/lane, two MFMAs per V operand, clamped
+    # unguarded loads, three batches in flight, next tile's loads before the stores) for 17-64 kept
+    "rotw_off": {"NKV_ROTW": 0},   # the rotation before r06
+    "rotw_w4": {"NKV_ROTW_W": 4},
+    "rotw_w16": {"NKV_ROTW_W": 16},
+    "rotw_u2": {"NKV_ROTW_U": 2},
+    "rotw_mb8": {"NKV_ROTW_MAX_MB": 8},
+    # timing-only diagnostics (wrong results), tools/experiments/rotw_diag.patch: 1 = L2-resident rows
+    # (issue / MFMA ceiling), 2 = VALU adds instead of MFMAs (access-pattern ceiling); APRE: V operands
+    # of a batch read from LDS before its first MFMA
+    "rotw_diag1": {"patch": "rotw_diag", "NKV_ROTW_DIAG": 1},
+    "rotw_diag2": {"patch": "rotw_diag", "NKV_ROTW_DIAG": 2},
+    "rotw_apre": {"patch": "rotw_diag", "NKV_ROTW_APRE": 1},
+    # the diagnostics above: the L2-resident MFMA stream runs at 9 TB/s-equivalent, the access pattern
+    # alone (no MFMA) at 5.3 -> the persistent grid's drift, not the MFMAs, limits 17-32 kept; row bands
+    "rotw_r0": {"NKV_ROTW_ROUNDS": 0},
+    "rotw_r1": {"NKV_ROTW_ROUNDS": 1},
+    "rotw_r4": {"NKV_ROTW_ROUNDS": 4},
+    "rotw_r8": {"NKV_ROTW_ROUNDS": 8},
+    "rotw_r2_diag2": {"patch": "rotw_diag", "NKV_ROTW_ROUNDS": 2, "NKV_ROTW_DIAG": 2},
+    # the LDS-staged rotation (k_rotate_glds, tools/experiments/rot_glds.patch: 1 KiB one-column
+    # LDS-DMA loads, MFMA fragments from LDS, outputs transposed through LDS into 1 KiB one-column
+    # stores): 5-15 % slower than the wide-load kernel at 20-64 kept columns, k = 64-200 (r06k), not
+    # adopted; in r06f-k the product's "base" was this kernel and "rotg_off" the wide-load one
+    "rot_glds": {"patch": "rot_glds"},
+    "rotg_d6": {"patch": "rot_glds", "NKV_ROTG_D": 6},
+    "rotg_d5": {"patch": "rot_glds", "NKV_ROTG_D": 5},
+    "rot_old": {"NKV_ROTW": 0},   # the rotation before round 6
+    "rw_ntst0": {"NKV_NT_ST": 0},   # cached stores (every streaming kernel)
+    "rw_nt0": {"NKV_NT": 0},        # cached loads
+    "rw_nt00": {"NKV_NT": 0, "NKV_NT_ST": 0},
 }
 
 
@@ -228,6 +259,9 @@ def run(names, E, rounds, js, only=None):
     nrm = torch.zeros(8, dtype=torch.float64, device=dev)
     N, Nw, nv = lay.N, lay.N_w, lay.n_v
     V = torch.eye(jmax, dtype=torch.float64, device=dev).flatten()  # rotation by I keeps Q bounded
+    if os.environ.get("NKV_TUNE_VRAND", "0") == "1":   # a dense orthogonal V (the MFMAs on real data,
+        # as a restart's Schur vectors; orthonormal columns keep the repeatedly rotated Q bounded)
+        V = torch.as_tensor(np.linalg.qr(np.random.default_rng(5).standard_normal((jmax, jmax)))[0].ravel(order="F").copy()).to(dev)
     hd = torch.zeros(2 * (jmax + 1), dtype=torch.float64, device=dev)
     f2 = torch.zeros(Lc.ld, dtype=torch.float64, device=dev)
     dgl = torch.full((Lc.ld,), 0.5, dtype=torch.float64, device=dev)
@@ -280,6 +314,8 @@ def run(names, E, rounds, js, only=None):
                           8.0 * (j + min(32, j)) * N),
             "rotate_64": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(64, j), st),
                           8.0 * (j + min(64, j)) * N),
+            **{f"rotate_{n}": ((lambda n=n: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, min(n, j), st)),
+                               8.0 * (j + min(n, j)) * N) for n in (20, 25, 40, 48)},
             "rotate_half": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 2), st),
                             8.0 * (j + max(1, j // 2)) * N),
             "rotate_part": (lambda: L.nkv_rotate_cols(Lp, Q.data_ptr(), j, V.data_ptr(), jmax, max(1, j // 6), st),
