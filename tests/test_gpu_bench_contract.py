@@ -151,3 +151,4 @@ def test_bench_two_ranks_with_restart_and_krylov_schur_legs(gpu):
     assert d1["restart"]["mstart"] == d2["restart"]["mstart"]
     assert d2["restart"]["rotate_kept_ms"] > 0 and d2["restart"]["rotate_full_ms"] > 0
     assert 0 < d2["restart"]["rotate_kept_steady_frac_hbm"] < 1
+    assert d2["restart"]["rotate_wide_kept"] >= 17 and 0 < d2["restart"]["rotate_wide_frac_hbm"] < 1
