@@ -182,6 +182,15 @@ VARIANTS = {
     "rw_ntst0": {"NKV_NT_ST": 0},   # cached stores (every streaming kernel)
     "rw_nt0": {"NKV_NT": 0},        # cached loads
     "rw_nt00": {"NKV_NT": 0, "NKV_NT_ST": 0},
+    # workgroup visits of NKV_ROTW_SPAN consecutive tiles (SPAN 16 = 4096 rows per column) in row-band
+    # launches (tools/experiments/rotw_span.patch): tools/write_streams.hip's plain shape gains 6 % from
+    # 16-64 bands of 4096-row tiles, the wide-load rotation within +-1 % (r06o): not adopted
+    "rotw_s16": {"patch": "rotw_span", "NKV_ROTW_SPAN": 16},
+    "rotw_s16_r1": {"patch": "rotw_span", "NKV_ROTW_SPAN": 16, "NKV_ROTW_ROUNDS": 1},
+    "rotw_s16_r2": {"patch": "rotw_span", "NKV_ROTW_SPAN": 16, "NKV_ROTW_ROUNDS": 2},
+    "rotw_s4_r4": {"patch": "rotw_span", "NKV_ROTW_SPAN": 4, "NKV_ROTW_ROUNDS": 4},
+    "rotw_s8_r2": {"patch": "rotw_span", "NKV_ROTW_SPAN": 8, "NKV_ROTW_ROUNDS": 2},
+    "rotw_s32_r1": {"patch": "rotw_span", "NKV_ROTW_SPAN": 32, "NKV_ROTW_ROUNDS": 1},
 }
 
 
