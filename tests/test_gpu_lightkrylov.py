@@ -43,7 +43,7 @@ def _dense(ctx, A, w):
     return M, W, idx
 
 
-@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+@pytest.mark.parametrize("mode", ["dcgs2"])
 def test_svds_matches_dense_weighted_svd(gpu, mode):
     ctx, w, d, vh, A = _setup()
     M, W, idx = _dense(ctx, A, w)
@@ -66,7 +66,7 @@ def test_svds_matches_dense_weighted_svd(gpu, mode):
     assert np.sqrt(ctx.dot(Av, Av, False)) < 1e-9 * r.sigma[0]
 
 
-@pytest.mark.parametrize("mode", ["dcgs2", "cgs2"])
+@pytest.mark.parametrize("mode", ["dcgs2"])
 def test_svds_rank_deficient_breakdown(gpu, mode):
     """A rank-3 operator (three nonzero diagonal entries, W-self-adjoint, so the singular values are
     |d_i|) with k=12: the bidiagonalisation is invariant after 4 steps.  svds detects it (the
