@@ -76,11 +76,12 @@ def test_pmc_traffic_splits_back_to_back_calls(tmp_path):
 def test_launch_model_matches_committed_traces():
     """The band counts the model derives for bench.py's layout (E=44,176) divide the dispatch counts
     of a committed full-size rocprofv3 trace into whole calls: the dual update and the diagonal
-    matvec once per Arnoldi step (as many calls as multi-dots), the 6-kept rotation 3 times."""
+    matvec once per Arnoldi step (as many calls as multi-dots), the 6-kept rotation 3 times, the
+    25-kept one (one dispatch per call) 3 times in the restart section + once in the restart leg."""
     lm = _tool("launch_model")
     rows = lm.rows_of_E(44176)
     calls = {}
-    with open(os.path.join(ROOT, "profiles", "r05ak_bench_n1_kernel_stats.csv")) as fh:
+    with open(os.path.join(ROOT, "profiles", "r06q_bench_n1_kernel_stats.csv")) as fh:
         for r in csv.DictReader(fh):
             calls[r["Name"]] = int(r["Calls"])
     n = {k: v for k, v in calls.items()}
@@ -91,6 +92,8 @@ def test_launch_model_matches_committed_traces():
     assert n[upd] == lm.dispatches_per_call(upd, rows) * n[dot2] == 16 * n[dot2]
     assert n[opd] == lm.dispatches_per_call(opd, rows) * n[dot2] == 6 * n[dot2]
     assert n[rotf] == 3 * lm.dispatches_per_call(rotf, rows) == 3 * 64
+    rotw = next(k for k in n if "k_rotate_wide<2, 8, 4>" in k)
+    assert n[rotw] == 4 * lm.dispatches_per_call(rotw, rows) == 4
 
 
 def _write_trace(path, seq):

@@ -11,6 +11,9 @@ profile tools can split a run of back-to-back dispatches of one kernel into call
   grid per launch, one launch when fewer than two bands;
 * ``k_rotate_few<NO, P, U>`` (nkv_rotate_cols, csrc/rotate.hip launch_rotate_few):
   NKV_ROTF_ROUNDS rounds of a min(tiles, NKV_ROTF_G) grid per launch;
+* ``k_rotate_wide<MB, W, U>`` (17-64 kept columns): one launch while NKV_ROTW_ROUNDS = 0 (the
+  default; a banded build's grid comes from the runtime occupancy query, so it is not modelled and
+  ``dispatches_per_call`` refuses it);
 * everything else: one dispatch per call.
 
 The knob values are read from the product sources (``#define NKV_...`` defaults), so a retuned
@@ -64,6 +67,8 @@ def dispatches_per_call(kernel_name: str, rows: int, kn: dict | None = None) -> 
         r = kn["NKV_STREAM_ROUNDS"]
         band = r * g if (r > 0 and chunks >= 2 * r * g) else max(chunks, 1)
         return max(1, math.ceil(chunks / band))
+    if _targs(kernel_name, "k_rotate_wide") is not None and kn.get("NKV_ROTW_ROUNDS", 0) > 0:
+        raise NotImplementedError("banded k_rotate_wide: the grid is the runtime occupancy query's")
     a = _targs(kernel_name, "k_rotate_few")
     if a is not None:
         P = int(a[1])
