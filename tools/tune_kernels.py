@@ -182,6 +182,11 @@ VARIANTS = {
     "rw_ntst0": {"NKV_NT_ST": 0},   # cached stores (every streaming kernel)
     "rw_nt0": {"NKV_NT": 0},        # cached loads
     "rw_nt00": {"NKV_NT": 0, "NKV_NT_ST": 0},
+    # the VALU few-column rotation past 16 kept columns (NO accumulators per row pair,
+    # tools/experiments/rotf_wide.patch): 11-60 % slower than the wide-load MFMA kernel at 20-32 kept,
+    # k = 64-200 (r06u), not adopted
+    "rotf32": {"patch": "rotf_wide", "NKV_ROTF_MAX": 32},
+    "rotf32_p2": {"patch": "rotf_wide", "NKV_ROTF_MAX": 32, "NKV_ROTF_P_WIDE": 2},
     # workgroup visits of NKV_ROTW_SPAN consecutive tiles (SPAN 16 = 4096 rows per column) in row-band
     # launches (tools/experiments/rotw_span.patch): tools/write_streams.hip's plain shape gains 6 % from
     # 16-64 bands of 4096-row tiles, the wide-load rotation within +-1 % (r06o): not adopted
