@@ -856,7 +856,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
         return fail(NKV_EINVAL, "NKV_X_IS_LAST: x is not column j-1 of Q");
     hipStream_t st = S(stream);
     const bool large = use_large_tiles(L);
-    const int P = large ? NKV_DC_PAIRS : NKV_PAIRS_SMALL;
+    const int P = large ? NKV_D2_PAIRS : NKV_PAIRS_SMALL;
     const int kTile = kThreads * P * 2;
     const int tpf = (int)(L->sv / kTile);
     // large problems: one block row walks every field of its tiles (weights read once per tile)
@@ -873,7 +873,7 @@ int nkv_block_dot2(const nkv_layout* L, const double* w, const double* Q, int j,
     if (tpf > 0) {
         const int xl = (flags & NKV_X_IS_LAST) ? 1 : 0;
         if (large)
-            hipLaunchKernelGGL(k_block_dot2<NKV_DC_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
+            hipLaunchKernelGGL(k_block_dot2<NKV_D2_PAIRS>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double), st,
                                Q, L->ld, j, x, y, w, L->sv, tpf, nf, xl, part, B);
         else
             hipLaunchKernelGGL(k_block_dot2<NKV_PAIRS_SMALL>, dim3(bx, gy), dim3(kThreads), 8 * j * sizeof(double),

@@ -127,6 +127,9 @@ static_assert(NKV_FUSE_SMALL_J >= 0 && NKV_FUSE_SMALL_J <= 16,
 #ifndef NKV_D2_U
 #define NKV_D2_U 2  // basis columns in flight in the two-vector multi-dot
 #endif
+#ifndef NKV_D2_PAIRS
+#define NKV_D2_PAIRS NKV_DC_PAIRS  // double2 per thread per tile in the two-vector multi-dot (large problems)
+#endif
 // The round-1 timing experiments (store skipping, grid-wide soft barriers, tile-interleaved and
 // field-major sweeps, XCD tile maps, buffer-store cache policies, register-budget schedules;
 // CHANGELOG.md, "What did not help") are not part of this file.  The knobs above change speed only.

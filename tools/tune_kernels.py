@@ -185,6 +185,13 @@ VARIANTS = {
     # the VALU few-column rotation past 16 kept columns (NO accumulators per row pair,
     # tools/experiments/rotf_wide.patch): 11-60 % slower than the wide-load MFMA kernel at 20-32 kept,
     # k = 64-200 (r06u), not adopted
+    # round 6: the multi-dot's L1 request queue is full (TA stalled by the TC 34 % of cycles, r06e):
+    # the same bytes in flight per CU spread over more waves with fewer loads each
+    "d2p4_b512": {"NKV_D2_PAIRS": 4, "NKV_D2_MAXB": 512},
+    "d2p4_b256": {"NKV_D2_PAIRS": 4},
+    "d2p2_b1024": {"NKV_D2_PAIRS": 2, "NKV_D2_MAXB": 1024},
+    "d2p8_u1_b512": {"NKV_D2_U": 1, "NKV_D2_MAXB": 512},
+    "d2p4_u4_b256": {"NKV_D2_PAIRS": 4, "NKV_D2_U": 4},
     "rotf32": {"patch": "rotf_wide", "NKV_ROTF_MAX": 32},
     "rotf32_p2": {"patch": "rotf_wide", "NKV_ROTF_MAX": 32, "NKV_ROTF_P_WIDE": 2},
     # workgroup visits of NKV_ROTW_SPAN consecutive tiles (SPAN 16 = 4096 rows per column) in row-band
