@@ -108,3 +108,21 @@ def test_shard_traffic_lookup(tmp_path, monkeypatch):
     assert t == 6.7e9 and src["file"] == os.path.join("profiles", "traffic_E5522.json") and src["E_shard"] == 5522
     assert bench.find_traffic("dcgs2_update", 11044, 128) == (None, None)
     assert bench.find_traffic("block_dot2", 5522, 128) == (None, None)
+
+
+def test_driver_launcher_two_ranks_one_line():
+    """The driver's own launcher (``python -m torch.distributed.run --nnodes=1 --nproc-per-node 2
+    --master-addr 127.0.0.1 --master-port P bench.py --gpus 2 ...``): the ranks leave the group, rank 0
+    prints ONE complete line, and torch.distributed.run's agent reports success.  (torch.distributed.run
+    also parses long options after the script name by prefix, so ``--m`` would be taken for its own.)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", NKV_BACKEND="gloo")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", _port(9), BENCH, "--gpus", "2", "--dry-line",
+                        "--E", "64", "--cpu-E", "8", "--cpu-E-1core", "8", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["world"] == 2 and d["cpu_baseline"]["value"] > 0 and d["roofline"]["kernel"] == "dcgs2_update"
